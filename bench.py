@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""Headline benchmark: the GA evaluation loop at population 65 536 per GPU.
+
+One step = one GA generation of the reference's eaSimple loop
+(main.py:165-170) on device:
+  1. evaluate every genome's 6 self-play games to termination
+     (pg_eval_population: Pong physics + both paddles' [6,64,3] MLPs, fused),
+  2. all-gather the fitness over ranks (RCCL; N > 1 only),
+  3. hall-of-fame update (top pop//4 of HoF + population),
+  4. selTournament(tournsize = pop//4) + varAnd(cxBlend, mutGaussian) on device.
+Weak scaling: every rank evaluates 65 536 genomes of an N x 65 536 population.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 through
+torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the env).
+Rank 0 prints ONE JSON line.  Data: synthetic N(0, 3) genomes (the
+"evolved" distribution of SURVEY 8d), seeded per rank layout.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "neuro-genetic-pong-self-play_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--pop", type=int, default=65536, help="genomes evaluated per GPU")
+    p.add_argument("--shape", default="6,64,3")
+    p.add_argument("--games", type=int, default=6)
+    p.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    p.add_argument("--group-lanes", type=int, default=0)
+    p.add_argument("--kernel", default="auto")
+    p.add_argument("--sigma", type=float, default=3.0)
+    p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from pong_amd import build as B
+    from pong_amd import device as D
+    from pong_amd import dist as PD
+    B.build()
+
+    shape = [int(v) for v in args.shape.split(",")]
+    dtype = torch.float64 if args.dtype == "float64" else torch.float32
+    n_local = args.pop
+    P = n_local * world
+    H = max(P // 4, 1)                 # HALL_OF_FAME_AMOUNT = POPULATION_SIZE // 4 (config.py:49-50)
+    tournsize = max(P // 4, 1)          # TOURNAMENT_SIZE (config.py:49)
+    ev = D.Evaluator(shape, dtype=dtype, device=dev, n_games=args.games, kernel=args.kernel,
+                     group_lanes=args.group_lanes)
+    G = ev.genes
+
+    # replicated population (identical on every rank: same seed), HoF = first H genomes
+    gen = torch.Generator(device=dev).manual_seed(args.seed)
+    pop = torch.randn((P, G), generator=gen, dtype=torch.float64, device=dev).mul_(args.sigma).to(dtype)
+    off = torch.empty_like(pop)
+    hof = pop[:H].clone()
+    hof_fit = torch.full((H,), -1e300, dtype=torch.float64, device=dev)
+    lo, hi = PD.shard_range(P, rank, world)
+    kind, opp, mult = ev.selfplay_schedule(hi - lo, H, offset=lo)
+    res_buf = None
+
+    cxpb, mutpb, alpha, mu, sigma, indpb = 0.9, 0.9, 0.9, 0.0, 0.9, 0.9  # config.py:36-42
+    ev_start = torch.cuda.Event(enable_timing=True)
+    ev_end = torch.cuda.Event(enable_timing=True)
+
+    def generation(g, timed):
+        nonlocal pop, off, hof, hof_fit, res_buf
+        if timed:
+            ev_start.record()
+        res, _ = ev.evaluate(pop[lo:hi], kind, opp, mult, opponents=hof, out=res_buf, validate=False)
+        if timed:
+            ev_end.record()
+        res_buf = res
+        fit = PD.gather_fitness(res.fitness, P) if world > 1 else res.fitness
+        # hall of fame: best H of (HoF, population)
+        cand = torch.cat([hof_fit, fit])
+        top = torch.topk(cand, H, sorted=False).indices
+        from_hof = top < H
+        new_hof = torch.empty_like(hof)
+        new_hof[from_hof] = hof[top[from_hof]]
+        new_hof[~from_hof] = pop[top[~from_hof] - H]
+        hof, hof_fit = new_hof, cand[top]
+        # selection + variation
+        chosen = D.select_tournament_ranked(fit, P, tournsize, seed=args.seed, generation=g)
+        off, _ = D.vary(pop, chosen, G, cxpb, mutpb, alpha, mu, sigma, indpb, seed=args.seed,
+                        generation=g, out=off)
+        pop, off = off, pop
+        return res
+
+    for w in range(args.warmup):
+        generation(w, False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    steps_local = 0
+    fwd_local = 0
+    slow_local = 0
+    kernel_ms = []
+    counters = []
+    for s in range(args.steps):
+        res = generation(args.warmup + s, True)
+        counters.append(res.counters.clone())
+        kernel_ms.append((ev_start, ev_end))
+        # events are reused: read this step's kernel time before the next record
+        torch.cuda.synchronize(dev)
+        kernel_ms[-1] = ev_start.elapsed_time(ev_end)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    for c in counters:
+        c = c.cpu()
+        steps_local += int(c[0])
+        fwd_local += int(c[1])
+        slow_local += int(c[2])
+
+    t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)],
+                     dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        steps_all, fwd_all, slow_all = float(tsum[1]), float(tsum[2]), float(tsum[3])
+        kernel_ms_mean = float(tsum[4]) / world / args.steps
+    else:
+        steps_all, fwd_all, slow_all = float(t[1]), float(t[2]), float(t[3])
+        kernel_ms_mean = float(t[4]) / args.steps
+
+    if rank == 0:
+        env_steps_per_s = steps_all / elapsed
+        ms_per_step = elapsed * 1000.0 / args.steps
+        # roofline of the dominant kernel (k_resident), per launch on rank 0's timing
+        flops_per_forward = 2.0 * G
+        fwd_per_launch = fwd_all / world / args.steps
+        steps_per_launch = steps_all / world / args.steps
+        achieved_tflops = fwd_per_launch * flops_per_forward / (kernel_ms_mean / 1e3) / 1e12
+        streaming_bytes = steps_per_launch * (2 * 4 * G + 128)   # SURVEY 8d accounting, GB-equivalent
+        out = {
+            "metric": "env-steps/sec (GA evaluation loop, self-play) + generations/sec at pop=65536 per GPU",
+            "value": env_steps_per_s,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "generations_per_sec": 1000.0 / ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 hidden + certified f64 argmax; genomes " + ("f64" if dtype == torch.float64 else "f32"),
+            "data": "synthetic N(0,%g) genomes, random-init [%s] MLPs, self-play vs hall of fame" % (args.sigma, args.shape),
+            "config": {"workload": "BASELINE config 3: population 65536 per GPU, MLP [6,64,3], 6 self-play games "
+                                   "per genome, device GA step (selTournament/varAnd/HoF)",
+                       "population": P, "population_per_gpu": n_local, "network_shape": shape,
+                       "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
+                       "parallelism": f"dp{world}" if world > 1 else "dp1",
+                       "env_steps_per_generation": steps_all / args.steps,
+                       "f64_redecisions_per_forward": slow_all / max(fwd_all, 1.0)},
+            "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved_tflops / F32_VECTOR_PEAK_TFLOPS,
+                         "traffic": None,
+                         "kernel": "k_resident (pg_eval_population)",
+                         "kernel_ms_per_launch": kernel_ms_mean,
+                         "flops_per_forward": flops_per_forward,
+                         "forwards_per_launch": fwd_per_launch,
+                         "streaming_equivalent_GBps": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9,
+                         "streaming_equivalent_frac_of_hbm": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9 / HBM_PEAK_GBS},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo):
+    """The CPU oracle (C restatement of the reference loop, f64 numpy_nn
+    arithmetic) on the same workload's first genomes, on the host cores."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    O.build()
+    genomes = pop[: 1 << 14].double().cpu().numpy()
+    opponents = hof.double().cpu().numpy()
+    k, o, m = kind.cpu().numpy(), opp.cpu().numpy(), mult.cpu().numpy()
+    steps, done, chunk = 0, 0, 256
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_baseline_seconds and done + chunk <= genomes.shape[0]:
+        r = O.eval_population(genomes[done:done + chunk], shape, k[done:done + chunk], o[done:done + chunk],
+                              m[done:done + chunk], opponents=opponents, n_threads=args.cpu_threads)
+        steps += int(r["frames"].sum())
+        done += chunk
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"{done} genomes x {args.games} games of the same self-play workload "
+                      f"({steps} env-steps in {dt:.1f} s, OpenMP over {args.cpu_threads} host threads)",
+            "cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

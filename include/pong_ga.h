@@ -1,0 +1,197 @@
+/*
+ * pong_ga.h -- C-ABI of the MI355X-native GA evaluation loop (libpong_ga.so).
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (n00b001/neuro-genetic-pong-self-play).  Every entry point takes plain
+ * pointers and sizes; all array arguments are DEVICE pointers owned by the
+ * caller (the Python host passes torch tensors' data_ptr()), and every call
+ * is ordered on the HIP stream passed in (NULL = the null stream).  The
+ * library keeps no device allocations between calls.  Errors: the functions
+ * return PG_OK (0) or a negative pg_status; pg_last_error() returns a
+ * thread-local message for the last failure.  Nothing throws across the ABI.
+ * Threading: one host thread per device; the caller selects the device.
+ *
+ * Entry point                    replaces (reference file:line)
+ * ------------------------------ ---------------------------------------------
+ * pg_eval_population             toolbox.map(toolbox.evaluate, invalid_ind)
+ *                                (ga.py:83 futures.map, main.py:176 register):
+ *                                evaluate() main.py:28-66 for a whole batch,
+ *                                each game = perform_episode main.py:69-112 with
+ *                                env.step main.py:77, find_stuff utils.py:14-19,
+ *                                get_actions main.py:138-154, inference
+ *                                utils.py:139-153, NeuralNetwork.run
+ *                                numpy_nn.py:120-137, keep_within_game_bounds
+ *                                utils.py:71-77, calculate_timeout_and_frames
+ *                                main.py:128-135, calculate_reward utils.py:104-109
+ * pg_forward                     NeuralNetwork.run numpy_nn.py:120-137 (batched)
+ * pg_physics_reset/pg_physics_step  env.reset()/env.step(action) main.py:56,77
+ *                                (the build's SoA Pong; the emulator is absent)
+ * pg_ga_select_tournament        tools.selTournament (ga.py:94; DEAP)
+ * pg_ga_vary                     algorithms.varAnd with tools.cxBlend (ga.py:89)
+ *                                and tools.mutGaussian (ga.py:91-92; DEAP)
+ */
+#ifndef PONG_GA_H
+#define PONG_GA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PG_ABI_VERSION 1
+#define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
+
+typedef enum pg_status {
+  PG_OK = 0,
+  PG_ERR_INVALID = -1,     /* bad argument (message in pg_last_error) */
+  PG_ERR_HIP = -2,         /* a HIP runtime call failed */
+  PG_ERR_UNSUPPORTED = -3  /* shape/option not supported by this build */
+} pg_status;
+
+typedef enum pg_dtype { PG_F32 = 0, PG_F64 = 1 } pg_dtype;
+
+/* Left-paddle opponent of one game (the genome always plays the right paddle,
+ * main.py:58 right_model). */
+typedef enum pg_opp_kind {
+  PG_OPP_HARDCODED = 0, /* HardcodedAi in the 2-player env     main.py:50-53 */
+  PG_OPP_ROM_CPU = 1,   /* 1-player env: built-in CPU opponent  main.py:39-40 */
+  PG_OPP_SCORE = 2,     /* ScoreHardcodedAi                     main.py:41-42 */
+  PG_OPP_NN = 3         /* NeuralNetwork of a hall-of-fame row  main.py:43-49 */
+} pg_opp_kind;
+
+typedef enum pg_precision {
+  /* f32 hidden math with a certified f64 argmax: every decision whose
+   * f32 error bound cannot prove the f64 argmax is recomputed in f64. */
+  PG_PREC_CERTIFIED = 0,
+  /* every forward in f64 (numpy_nn's arithmetic, sequential sums) */
+  PG_PREC_F64 = 1
+} pg_precision;
+
+typedef enum pg_kernel {
+  PG_KERNEL_AUTO = 0,
+  PG_KERNEL_GENERAL = 1,  /* one wave per game, f64, any NETWORK_SHAPE */
+  PG_KERNEL_RESIDENT = 2  /* weights resident in registers, [6, H<=256, 2..4] */
+} pg_kernel;
+
+/* NETWORK_SHAPE (config.py:30-32) + BIAS (config.py:34) + genome storage type. */
+typedef struct pg_net {
+  int32_t n_nodes;               /* len(NETWORK_SHAPE), >= 2 */
+  int32_t nodes[PG_MAX_NODES];   /* nodes[0] = 6 for the game loop */
+  int32_t bias;                  /* 1 = BIAS, weight rows are (in + 1) wide */
+  int32_t dtype;                 /* pg_dtype of genomes and opponents */
+} pg_net;
+
+typedef struct pg_eval_args {
+  pg_net net;
+  int32_t n_genomes;             /* rows of genomes evaluated by this call (>= 0) */
+  int32_t n_games;               /* GAMES_TO_PLAY (config.py:46), 1..64 */
+  const void *genomes;           /* [n_genomes, genome_stride] (net.dtype) */
+  int64_t genome_stride;         /* elements between genome rows, >= gene count */
+  const void *opponents;         /* [n_opponents, opponent_stride]: hall-of-fame genomes */
+  int64_t opponent_stride;
+  int32_t n_opponents;
+  int32_t precision;             /* pg_precision */
+  const int32_t *game_kind;      /* [n_genomes, n_games] pg_opp_kind */
+  const int32_t *game_opp;       /* [n_genomes, n_games] opponent row (PG_OPP_NN) */
+  const double *game_mult;       /* [n_genomes, n_games] right_score_multiplier */
+  uint64_t seed;                 /* physics seed base (config.PHYSICS_SEED) */
+  /* outputs, device */
+  double *fitness;               /* [n_genomes]  evaluate()[0] = sum(rewards)/n_games */
+  double *rewards;               /* [n_genomes, n_games] perform_episode() */
+  int32_t *scores;               /* [n_genomes, n_games, 2] final score1, score2 */
+  int32_t *frames;               /* [n_genomes, n_games] env.step calls */
+  double *total_frames;          /* [n_genomes, n_games] main.py:73 accumulator */
+  int32_t *status;               /* [n_genomes] 1 = ZeroDivisionError in calculate_reward */
+  uint64_t *counters;            /* optional [4]: env steps, NN forwards, f64 re-decisions, games */
+  uint8_t *trace;                /* optional [trace_games, trace_cap] per-frame action codes */
+  int32_t trace_games;           /* games (genome-major index g = i*n_games + game) traced */
+  int32_t trace_cap;
+  int32_t kernel;                /* pg_kernel */
+  int32_t group_lanes;           /* resident kernel lanes per game (4..64), 0 = auto */
+  void *workspace;               /* device scratch of pg_eval_workspace_bytes() bytes */
+  size_t workspace_bytes;
+} pg_eval_args;
+
+/* Trace byte: right_code | left_code << 2 | ball_visible << 4, where a code is
+ * 0 = [0,0], 1 = [1,0] (up), 2 = [0,1] (down): the action written into
+ * action[4:6] / action[6:8] after that frame (main.py:91-92). */
+
+typedef struct pg_forward_args {
+  pg_net net;
+  int32_t n;                     /* forward passes */
+  const void *genomes;           /* [*, genome_stride] (net.dtype) */
+  int64_t genome_stride;
+  const int32_t *genome_index;   /* [n] genome row of pass i; NULL = row i */
+  const double *x;               /* [n, nodes[0]] inputs */
+  int32_t precision;             /* pg_precision */
+  int32_t *index;                /* [n] np.argmax of the output activations */
+  double *act;                   /* optional [n, nodes[last]] output activations */
+  uint64_t *counters;            /* optional [4], as pg_eval_args */
+} pg_forward_args;
+
+/* Struct-of-arrays game state: int32 [PG_STATE_FIELDS, n], field f of game i
+ * at state[f * n + i]; 64 bytes per game. */
+enum {
+  PG_S_BALL_X = 0, PG_S_BALL_Y, PG_S_BALL_VX, PG_S_BALL_VY, PG_S_BALL_VISIBLE,
+  PG_S_SERVE_TIMER, PG_S_SERVE_DIR, PG_S_HITS, PG_S_POINT, PG_S_LEFT_Y, PG_S_RIGHT_Y,
+  PG_S_SCORE1, PG_S_SCORE2, PG_S_ONE_PLAYER, PG_S_SEED_LO, PG_S_SEED_HI,
+  PG_STATE_FIELDS
+};
+
+/* GA step on device (DEAP semantics, counter-based RNG): see pg_ga_vary. */
+typedef struct pg_ga_args {
+  int32_t n;                     /* population size */
+  int64_t genes;                 /* genes per genome */
+  int32_t dtype;                 /* pg_dtype of both genome buffers */
+  const void *parents;           /* [n_parents, stride] current population */
+  int64_t stride;
+  int32_t n_parents;
+  const int32_t *chosen;         /* [n] parent row of offspring slot i (selection) */
+  void *offspring;               /* [n, stride] output */
+  uint8_t *invalid;              /* [n] 1 = fitness invalidated (varied) */
+  double cxpb, mutpb;            /* CROSSOVER_BLEND_PROBABILITY, GAUSSIAN_MUTATION_PROBABILITY */
+  double alpha;                  /* CROSSOVER_BLEND_ALPHA */
+  double mu, sigma, indpb;       /* GAUSSIAN_MUTATION_MEAN/SIGMA, PROBABILITY_OF_MUTATING_A_SINGLE_GENE */
+  uint64_t seed;                 /* RNG key: (seed, generation) */
+  uint64_t generation;
+} pg_ga_args;
+
+typedef struct pg_select_args {
+  int32_t n_pop;                 /* individuals to choose from */
+  int32_t k;                     /* picks (len(population)) */
+  int32_t tournsize;             /* TOURNAMENT_SIZE (config.py:49) */
+  const double *fitness;         /* [n_pop] */
+  int32_t *chosen;               /* [k] output: row of the winner of tournament j */
+  uint64_t seed;
+  uint64_t generation;
+} pg_select_args;
+
+const char *pg_version(void);
+int32_t pg_abi_version(void);
+const char *pg_last_error(void);
+/* Number of visible HIP devices (>= 0), or a negative pg_status. */
+int32_t pg_device_count(void);
+size_t pg_eval_workspace_bytes(const pg_eval_args *args);
+int32_t pg_gene_count(const pg_net *net);
+
+int32_t pg_eval_population(const pg_eval_args *args, void *stream);
+int32_t pg_forward(const pg_forward_args *args, void *stream);
+int32_t pg_physics_reset(int32_t *state, int32_t n, const uint64_t *seeds,
+                         const int32_t *one_player, void *stream);
+/* actions [n]: bit0 right up, bit1 right down, bit2 left up, bit3 left down */
+int32_t pg_physics_step(int32_t *state, int32_t n, const uint8_t *actions, void *stream);
+int32_t pg_ga_select_tournament(const pg_select_args *args, void *stream);
+/* selTournament for large tournsize by rank sampling: the winner of a
+ * tournament of t draws with replacement has ascending rank floor(n V^(1/t))
+ * (V uniform), ties resolved uniformly -- the same distribution as the
+ * draw-by-draw tournament.  sorted_fitness ascending, order[r] = row of rank r. */
+int32_t pg_ga_select_tournament_ranked(const pg_select_args *args, const double *sorted_fitness,
+                                       const int32_t *order, void *stream);
+int32_t pg_ga_vary(const pg_ga_args *args, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PONG_GA_H */

@@ -1,0 +1,207 @@
+// pg_device.hpp -- device-side building blocks of the GA evaluation loop for
+// gfx950 (MI355X): the struct-of-arrays Pong stepper, the observation
+// features, the scripted opponents and wave-level reductions.
+//
+// Reference behaviour each piece reproduces is cited inline (file:line in
+// n00b001/neuro-genetic-pong-self-play).  The physics is the build's own
+// (DESIGN.md "Physics"): the reference steps the absent gym-retro emulator.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pg {
+
+// ---- playfield geometry: the 160x160 crop (rows 34..193) of obs.npy ----
+constexpr int kFieldW = 160;
+constexpr int kFieldH = 160;
+constexpr int kPaddleH = 16;
+constexpr int kPaddleW = 4;
+constexpr int kLeftPaddleX = 16;    // columns 16..19
+constexpr int kRightPaddleX = 140;  // columns 140..143
+constexpr int kBallH = 4;
+constexpr int kBallW = 2;
+constexpr int kPaddleYMin = -8;
+constexpr int kPaddleYMax = 152;
+constexpr int kPaddleSpeed = 3;
+constexpr int kCpuSpeed = 2;
+constexpr int kServeDelay = 30;
+constexpr int kBallVx0 = 2;
+constexpr int kBallVxMax = 4;
+constexpr int kDoneScore = 21;
+// ---- episode constants (config.py) ----
+constexpr int kWinScore = 3;          // WIN_SCORE config.py:53
+constexpr int kTimeoutThresh = 2000;  // TIMEOUT_THRESH config.py:28
+
+enum : int { kOppHard = 0, kOppRomCpu = 1, kOppScore = 2, kOppNN = 3 };
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Physics seed of game slot g (main.py:33): independent of the genome, as the
+// emulator started from a state file is deterministic.
+__host__ __device__ inline uint64_t game_seed(uint64_t base, int g) {
+  return splitmix64(base ^ (0xA24BAED4963EE407ull * (uint64_t)(g + 1)));
+}
+
+__device__ inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// One game's state: 16 x 32-bit words, the SoA row of pg_physics_* (64 B).
+struct Pong {
+  int bx, by, vx, vy, vis, timer, dir, hits, point, lpy, rpy, s1, s2, one_player;
+  uint64_t seed;
+
+  __device__ void reset(uint64_t s, int one_p) {
+    bx = 79; by = 78; vx = 0; vy = 0; vis = 0; timer = kServeDelay; dir = 1; hits = 0; point = 0;
+    lpy = 72; rpy = 72; s1 = 0; s2 = 0; one_player = one_p; seed = s;
+  }
+
+  __device__ bool done() const { return s1 >= kDoneScore || s2 >= kDoneScore; }
+
+  __device__ static int move(int y, int code, int speed) {
+    // code: 0 = [0,0], 1 = [1,0] up, 2 = [0,1] down, 3 = [1,1] (no motion)
+    y += (code == 1) ? -speed : ((code == 2) ? speed : 0);
+    return clampi(y, kPaddleYMin, kPaddleYMax);
+  }
+
+  // env.step(action) (main.py:77): right [up,down] = action[4:6], left = action[6:8].
+  __device__ void step(int right_code, int left_code) {
+    rpy = move(rpy, right_code, kPaddleSpeed);
+    if (one_player) {
+      int code = 0;
+      if (vis) {
+        const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
+        code = (bc2 < pc2 - 4) ? 1 : ((bc2 > pc2 + 4) ? 2 : 0);
+      }
+      lpy = move(lpy, code, kCpuSpeed);
+    } else {
+      lpy = move(lpy, left_code, kPaddleSpeed);
+    }
+    if (!vis) {
+      if (timer > 0) timer -= 1;
+      if (timer == 0 && !done()) serve();
+      return;
+    }
+    int nx = bx + vx, ny = by + vy, nvx = vx, nvy = vy;
+    constexpr int ymax = kFieldH - kBallH;
+    if (ny < 0) {
+      ny = -ny;
+      nvy = -nvy;
+    } else if (ny > ymax) {
+      ny = 2 * ymax - ny;
+      nvy = -nvy;
+    }
+    constexpr int lface = kLeftPaddleX + kPaddleW, rface = kRightPaddleX;
+    const bool to_left = (vx < 0) && (nx <= lface - 1);
+    const bool to_right = (vx > 0) && (nx + kBallW - 1 >= rface);
+    if (to_left || to_right) {
+      const int py = to_left ? lpy : rpy;
+      if (ny <= py + kPaddleH - 1 && ny + kBallH - 1 >= py) {  // bounce
+        hits += 1;
+        int mag = kBallVx0 + hits / 4;
+        mag = mag > kBallVxMax ? kBallVxMax : mag;
+        nx = to_left ? lface : rface - kBallW;
+        nvx = to_left ? mag : -mag;
+        nvy = (2 * (ny - py) - 12) / 6;  // truncation toward zero
+      } else {  // miss: the other side scores, the ball disappears until the next serve
+        if (to_left) { s2 += 1; dir = -1; } else { s1 += 1; dir = 1; }
+        vis = 0;
+        timer = kServeDelay;
+        return;
+      }
+    }
+    bx = nx; by = ny; vx = nvx; vy = nvy;
+  }
+
+  __device__ void serve() {
+    const uint64_t r = splitmix64(seed ^ ((uint64_t)(point + 1) * 0xD1B54A32D192ED03ull));
+    const int sel = (int)((r >> 32) & 3u);
+    bx = 79;
+    by = 40 + (int)(r % 77u);
+    vy = sel < 2 ? sel - 2 : sel - 1;  // {-2, -1, 1, 2}
+    vx = dir * kBallVx0;
+    hits = 0;
+    vis = 1;
+    point += 1;
+  }
+};
+
+// Doubled centroid row of a paddle clipped to rows [0,160): what
+// get_rect_quickly (utils.py:60-68) returns for the rendered rectangle, x2.
+__device__ inline int paddle_c2(int py) {
+  const int lo = py < 0 ? 0 : py;
+  const int hi = py + kPaddleH - 1 > kFieldH - 1 ? kFieldH - 1 : py + kPaddleH - 1;
+  return lo + hi;
+}
+
+// keep_within_game_bounds_please (utils.py:71-77): centroid < 16 -> down,
+// > 144 -> up.  In doubled units: c2 < 32, c2 > 288.
+__device__ inline int clamp_action(int c2, int code) {
+  return c2 < 32 ? 2 : (c2 > 2 * (kFieldH - 16) ? 1 : code);
+}
+
+// HardcodedAi.run (dumb_ais.py:2-8) on inference() features: compares
+// ball_y/160 (x[1]) with me/160 (x[4]); the /160 is monotone, so the doubled
+// integer centroids compare the same way.
+__device__ inline int hardcoded(int by2, int me2) { return by2 < me2 ? 1 : (by2 > me2 ? 2 : 0); }
+
+// argmax index -> action code (numpy_nn.py:131-137; index >= 2 -> no-op, the
+// build's extension for 3-output networks).
+__device__ inline int index_to_code(int idx) { return idx == 0 ? 1 : (idx == 1 ? 2 : 0); }
+
+// ---- wave-level helpers ----
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the L lanes of an aligned lane group; every lane of the group gets
+// the bitwise-identical total (each butterfly/mirror step adds the same two
+// operands in both partner lanes, and IEEE addition commutes).
+template <int L>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (L >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  if constexpr (L >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  if constexpr (L >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror: quad <-> quad
+  if constexpr (L >= 16) v += dpp_mov<0x140>(v); // row_mirror: half-row <-> half-row
+  if constexpr (L >= 32) v += __shfl_xor(v, 16, 64);
+  if constexpr (L >= 64) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+template <int L>
+__device__ __forceinline__ float group_max(float v) {
+  if constexpr (L >= 2) v = fmaxf(v, dpp_mov<0xB1>(v));
+  if constexpr (L >= 4) v = fmaxf(v, dpp_mov<0x4E>(v));
+  if constexpr (L >= 8) v = fmaxf(v, dpp_mov<0x141>(v));
+  if constexpr (L >= 16) v = fmaxf(v, dpp_mov<0x140>(v));
+  if constexpr (L >= 32) v = fmaxf(v, __shfl_xor(v, 16, 64));
+  if constexpr (L >= 64) v = fmaxf(v, __shfl_xor(v, 32, 64));
+  return v;
+}
+
+// Make a group-uniform value provably wave-uniform when the group is the whole
+// wave (lets hipcc keep the game state in SGPRs and branch on the scalar unit).
+template <int L>
+__device__ __forceinline__ int uniformize(int v) {
+  if constexpr (L == 64) return __builtin_amdgcn_readfirstlane(v);
+  return v;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// numpy's sigmoid 1 / (1 + np.e ** -x) (numpy_nn.py:22-23) in f64; np.e is the
+// double nearest e.  Plain IEEE ops in this order; pow is the only libm call.
+__device__ __forceinline__ double sigmoid_f64(double z) {
+  return 1.0 / __dadd_rn(1.0, pow(2.718281828459045, -z));
+}
+
+}  // namespace pg

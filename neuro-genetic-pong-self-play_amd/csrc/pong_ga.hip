@@ -1,0 +1,1040 @@
+// pong_ga.hip -- MI355X (gfx950) kernels and the C-ABI of libpong_ga.so.
+//
+// The hot path: evaluate() (main.py:28-66) for a whole population in one
+// launch.  Every game (perform_episode, main.py:69-112) runs to termination
+// inside the kernel: the Pong state and both networks' weights stay in
+// registers for the whole episode, so HBM is touched once per game (weights
+// in, results out) instead of once per frame.  See DESIGN.md.
+//
+//   k_resident<L,U,O,WT>  [6, H<=L*U, O] networks: an aligned group of L lanes
+//                         plays one game; lane l holds hidden units l, l+L, ..
+//                         (U per lane) of both paddles' networks in VGPRs; the
+//                         output dot products are DPP/shuffle group reductions.
+//                         f32 math with a certified f64 argmax (see certify()).
+//   k_general<WT>         any NETWORK_SHAPE, one wave per game, f64 numpy_nn
+//                         arithmetic with activations staged in LDS.
+//   k_fitness             sum(all_rewards) / GAMES_TO_PLAY in the reference order.
+//   k_forward_*           NeuralNetwork.run batched (parity entry point).
+//   k_physics_*           the SoA Pong stepper on its own.
+//   k_select / k_vary     DEAP selTournament / varAnd(cxBlend, mutGaussian).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/pong_ga.h"
+#include "pg_device.hpp"
+
+#ifndef PG_VERSION_STRING
+#define PG_VERSION_STRING "pong_ga 0.1.0 (gfx950)"
+#endif
+
+namespace pg {
+
+// --------------------------------------------------------------- errors ----
+static thread_local std::string g_last_error;
+
+static int32_t fail(int32_t code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define PG_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(PG_ERR_HIP, "%s failed: %s", #call, hipGetErrorString(e_));        \
+  } while (0)
+
+// ------------------------------------------------------- kernel params ----
+struct EvalParams {
+  const void *genomes;
+  const void *opponents;
+  const int32_t *rows;  // unused (reserved)
+  const int32_t *kind;
+  const int32_t *opp;
+  const double *mult;
+  double *rewards;
+  int32_t *scores;
+  int32_t *frames;
+  double *total_frames;
+  int32_t *status_game;  // [n*games] scratch: zero-division per game
+  uint64_t *counters;
+  uint8_t *trace;
+  unsigned int *work;    // dynamic game counter (workspace)
+  int64_t gstride, ostride;
+  uint64_t seed;
+  int n_genomes, n_games, total;
+  int trace_games, trace_cap;
+  int nodes[PG_MAX_NODES];
+  int n_nodes, bias, max_width;
+};
+
+// Results of one finished game: perform_episode's return value and the
+// bookkeeping around it (main.py:108-112, utils.py:104-109).
+__device__ inline void finish_game(const EvalParams &p, int w, const Pong &st, int frames, int total) {
+  const double mult = p.mult[w];
+  double reward = 0.0;
+  int zero_div = 0;
+  if (st.s1 != st.s2) {
+    const double tf = (double)total;
+    if (tf == 0.0) {
+      zero_div = 1;
+      reward = __builtin_nan("");
+    } else {
+      // ((my - enemy) + my * mult) / (total_frames / 100.0), no contraction
+      const double diff = (double)(st.s2 - st.s1);
+      const double bonus = __dmul_rn((double)st.s2, mult);
+      reward = __dadd_rn(diff, bonus) / (tf / 100.0);
+    }
+  }
+  p.rewards[w] = reward;
+  p.scores[2 * w] = st.s1;
+  p.scores[2 * w + 1] = st.s2;
+  p.frames[w] = frames;
+  p.total_frames[w] = (double)total;
+  p.status_game[w] = zero_div;
+}
+
+// ===================================================== general (f64) path ==
+// One forward pass of NeuralNetwork.run (numpy_nn.py:120-137) by one wave, in
+// f64 with numpy_nn's operation order per unit (sequential dot product over
+// [inputs..., 1]); cur holds the input vector (with the trailing 1 if bias).
+// Returns the argmax index; cur/nxt are LDS buffers of max_width + 1 doubles.
+template <typename WT>
+__device__ int forward_f64_wave(const WT *__restrict__ w, const int *nodes, int n_nodes, int b,
+                                double *&cur, double *&nxt, int lane) {
+  long off = 0;
+  for (int l = 0; l + 1 < n_nodes; ++l) {
+    const int nin = nodes[l], nout = nodes[l + 1], cols = nin + b;
+    for (int j = lane; j < nout; j += 64) {
+      const WT *row = w + off + (long)j * cols;
+      double z = 0.0;
+      for (int i = 0; i < cols; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], cur[i]));
+      nxt[j] = sigmoid_f64(z);
+    }
+    if (b && lane == 0) nxt[nout] = 1.0;
+    wave_lds_sync();
+    off += (long)cols * nout;
+    double *t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+  const int n_out = nodes[n_nodes - 1];
+  int best = 0;
+  for (int j = 1; j < n_out; ++j)
+    if (cur[j] > cur[best]) best = j;  // np.argmax: first maximum
+  return best;
+}
+
+// Features of utils.inference (utils.py:139-153) in f64 from doubled
+// centroids k: value = (k / 2) / 160, exactly the reference's rounding.
+__device__ inline double feat64(int k) { return __dmul_rn(0.5, (double)k) / 160.0; }
+__device__ inline double feat64_flip(int k) { return (160.0 - __dmul_rn(0.5, (double)k)) / 160.0; }
+
+template <typename WT>
+__global__ __launch_bounds__(64) void k_general(EvalParams p) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x;
+  const int W = p.max_width + 1;
+  double *bufA = lds, *bufB = lds + W;
+  const WT *genomes = (const WT *)p.genomes;
+  const WT *opponents = (const WT *)p.opponents;
+  uint64_t c_steps = 0, c_fwd = 0, c_games = 0;
+  for (;;) {
+    int w = 0;
+    if (lane == 0) w = (int)atomicAdd(p.work, 1u);
+    w = __builtin_amdgcn_readfirstlane(w);
+    if (w >= p.total) break;
+    const int i = w / p.n_games, g = w % p.n_games;
+    const int kind = p.kind[w];
+    const WT *gr = genomes + (long)i * p.gstride;
+    const WT *gl = (kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
+    Pong st;
+    st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
+    int act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
+    for (;;) {
+      const int s1b = st.s1, s2b = st.s2;
+      const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
+      st.step(act_r, act_l);
+      frames += 1;
+      const int vis = st.vis;
+      const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
+      const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
+      int left = 0, right = 0;
+      if (vis) {  // get_actions main.py:143-150
+        const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
+        if (kind == kOppNN) {
+          double *cur = bufA, *nxt = bufB;
+          if (lane == 0) {
+            cur[0] = feat64_flip(bx2); cur[1] = feat64(by2); cur[2] = feat64_flip(lbx2);
+            cur[3] = feat64(lby2); cur[4] = feat64(lc2); cur[5] = feat64(rc2);
+            if (p.bias) cur[6] = 1.0;
+          }
+          wave_lds_sync();
+          left = index_to_code(forward_f64_wave(gl, p.nodes, p.n_nodes, p.bias, cur, nxt, lane));
+          wave_lds_sync();
+          c_fwd += 1;
+        } else if (kind == kOppScore) {
+          left = (st.s1 <= st.s2) ? hardcoded(by2, lc2) : 0;
+        } else {
+          left = hardcoded(by2, lc2);
+        }
+        double *cur = bufA, *nxt = bufB;
+        if (lane == 0) {
+          cur[0] = feat64(bx2); cur[1] = feat64(by2); cur[2] = feat64(lbx2);
+          cur[3] = feat64(lby2); cur[4] = feat64(rc2); cur[5] = feat64(lc2);
+          if (p.bias) cur[6] = 1.0;
+        }
+        wave_lds_sync();
+        right = index_to_code(forward_f64_wave(gr, p.nodes, p.n_nodes, p.bias, cur, nxt, lane));
+        wave_lds_sync();
+        c_fwd += 1;
+      }
+      act_l = clamp_action(lc2, left);
+      act_r = clamp_action(rc2, right);
+      if (p.trace && w < p.trace_games && frames <= p.trace_cap && lane == 0)
+        p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+      if (frames > 1) {  // calculate_timeout_and_frames main.py:128-135
+        if (st.s1 == s1b && st.s2 == s2b) {
+          timeout += 1;
+        } else {
+          total += timeout;
+          timeout = 0;
+        }
+      }
+      if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) break;
+    }
+    c_steps += frames;
+    c_games += 1;
+    if (lane == 0) finish_game(p, w, st, frames, total);
+  }
+  if (p.counters && lane == 0 && c_games) {
+    atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)c_steps);
+    atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
+    atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
+  }
+}
+
+// ================================================== resident (fast) path ==
+constexpr float kU = 5.9604644775390625e-8f;  // 2^-24, f32 unit roundoff
+
+template <int U, int O>
+struct Net {
+  float w1[U][7];  // hidden unit j = lane + L*u: 6 input weights + bias weight
+  float w2[U][O];  // output weights of that hidden unit
+  float c[O];      // output biases
+  float e[O];      // certified error bound of each output pre-activation
+};
+
+// Loads the [6, H, O] genome's weights for this lane (numpy_nn.py:52-69
+// layout: layer l is a row-major (out, in + bias) block, bias column last) and
+// computes the error bound E_o of the f32 output pre-activations:
+//   hidden a_j error  <= 11u R_j           (R_j = sum_i |W1_ji| incl. bias; |x_i| <= 1)
+//   sigmoid error     <= 2.75u R_j + 4.5u  (v_exp_f32/v_rcp_f32 ~1 ulp, slope <= 1/4)
+//   output z_o error  <= sum_j |W2_oj| (3u R_j + 5u) + 13u (sum_j |W2_oj| + |c_o|)
+// and keeps twice that (DESIGN.md "Certified argmax").
+template <int L, int U, int O, typename WT>
+__device__ void load_net(Net<U, O> &n, const WT *__restrict__ g, int H, int b, int lig) {
+  const int cols = 6 + b;
+  const long off2 = (long)H * cols;
+  float acc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = lig + L * u;
+    const bool ok = j < H;
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const bool use = ok && (i < 6 || b);
+      n.w1[u][i] = use ? (float)g[(long)j * cols + i] : 0.f;
+      r += fabsf(n.w1[u][i]);
+    }
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      n.w2[u][o] = ok ? (float)g[off2 + (long)o * (H + b) + j] : 0.f;
+      acc[o] += fabsf(n.w2[u][o]) * (3.f * r + 18.f);
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    n.c[o] = b ? (float)g[off2 + (long)o * (H + b) + H] : 0.f;
+    n.e[o] = 2.f * kU * (group_sum<L>(acc[o]) + 13.f * fabsf(n.c[o]));
+  }
+}
+
+__device__ __forceinline__ float sigmoid_f32(float a) {
+  // 1 / (1 + e^-a) with v_exp_f32 (2^x) and v_rcp_f32, ~1 ulp each
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a * -1.4426950408889634f));
+}
+
+template <int L, int U, int O>
+__device__ __forceinline__ void forward_f32(const Net<U, O> &n, const float x[6], float z[O]) {
+  float acc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float a = n.w1[u][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a = fmaf(n.w1[u][i], x[i], a);
+    const float s = sigmoid_f32(a);
+#pragma unroll
+    for (int o = 0; o < O; ++o) acc[o] = fmaf(n.w2[u][o], s, acc[o]);
+  }
+#pragma unroll
+  for (int o = 0; o < O; ++o) z[o] = group_sum<L>(acc[o]) + n.c[o];
+}
+
+// Certified argmax of S(z) = 1/(1 + pow(e, -z)) in f64 (numpy_nn.py:22-23,131)
+// given |z_true - z[o]| <= e[o].  S is exactly 1.0 iff z >= 53 ln 2 =
+// 36.73680056967710 (then every saturated output ties and the first wins);
+// below that, S rounds onto plateaus whose width in z is at most
+// 2^-52 (e^z + 1) (x4 margin below).  Returns -1 when the bound cannot prove
+// the f64 decision; the caller then recomputes the forward pass in f64.
+template <int O>
+__device__ __forceinline__ int certify(const float z[O], const float e[O]) {
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    if (!(z[o] + e[o] < 36.7367f)) return (z[o] - e[o] > 36.7369f) ? o : -1;
+  }
+  int w = 0;
+#pragma unroll
+  for (int o = 1; o < O; ++o)
+    if (z[o] > z[w]) w = o;
+  const float lo = z[w] - e[w];
+  const float tw = 8.8817842e-16f * (__expf(z[w] + e[w]) + 1.0f);
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < O; ++k)
+    if (k != w) ok = ok && (lo - (z[k] + e[k]) > tw);
+  return ok ? w : -1;
+}
+
+// The f64 re-decision of one forward pass by the L lanes of a group, in
+// numpy_nn's order (sequential dot products), hidden activations in LDS.
+// Returns the argmax; writes the output activations to act (group LDS) too.
+template <int L, int U, int O, typename WT>
+__device__ int forward_f64_group(const WT *__restrict__ g, int H, int b, const double x[6], double *lds,
+                                 int lig) {
+  const int cols = 6 + b;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = lig + L * u;
+    if (j < H) {
+      const WT *row = g + (long)j * cols;
+      double z = 0.0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], x[i]));
+      if (b) z = __dadd_rn(z, (double)row[6]);
+      lds[j] = sigmoid_f64(z);
+    }
+  }
+  wave_lds_sync();
+  if (lig < O) {
+    const WT *v = g + (long)H * cols + (long)lig * (H + b);
+    double z = 0.0;
+    for (int j = 0; j < H; ++j) z = __dadd_rn(z, __dmul_rn((double)v[j], lds[j]));
+    if (b) z = __dadd_rn(z, (double)v[H]);
+    lds[H + 1 + lig] = sigmoid_f64(z);
+  }
+  wave_lds_sync();
+  int best = 0;
+#pragma unroll
+  for (int o = 1; o < O; ++o)
+    if (lds[H + 1 + o] > lds[H + 1 + best]) best = o;
+  return best;
+}
+
+template <int L, int U, int O, typename WT>
+__device__ __forceinline__ int decide(const Net<U, O> &n, const WT *g, int H, int b, const int k[6],
+                                      double *lds, int lig, uint32_t &slow) {
+  float x[6], z[O];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = (float)k[i] * 0.003125f;  // k / 320, <= 2u relative error
+  forward_f32<L, U, O>(n, x, z);
+  int idx = certify<O>(z, n.e);
+  if (idx < 0) {  // group-uniform: every lane of the group holds the same z
+    double xd[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) xd[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
+    idx = forward_f64_group<L, U, O, WT>(g, H, b, xd, lds, lig);
+    wave_lds_sync();
+    slow += 1;
+  }
+  return index_to_code(idx);
+}
+
+template <int L>
+__device__ __forceinline__ int group_broadcast(int v, int leader_lane) {
+  if constexpr (L == 64) return __builtin_amdgcn_readfirstlane(v);
+  return __shfl(v, leader_lane, 64);
+}
+
+template <int L, int U, int O, typename WT>
+__global__ __launch_bounds__(256) void k_resident(EvalParams p) {
+  constexpr int GPB = 256 / L;  // game groups per block
+  const int H = p.nodes[1];
+  const int b = p.bias;
+  extern __shared__ double lds_all[];
+  const int lane64 = threadIdx.x & 63;
+  const int lig = threadIdx.x & (L - 1);
+  const int grp = threadIdx.x / L;
+  const int leader = lane64 & ~(L - 1);
+  double *lds = lds_all + grp * (H + 1 + O + 1);
+  const WT *genomes = (const WT *)p.genomes;
+  const WT *opponents = (const WT *)p.opponents;
+
+  Net<U, O> nr, nl;
+  Pong st;
+  int w = 0, kind = 0, g = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
+  const WT *gr = nullptr, *gl = nullptr;
+  uint32_t slow = 0, c_fwd = 0;
+  uint64_t c_steps = 0, c_games = 0;
+
+  auto start_game = [&]() {
+    int ww = 0;
+    if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
+    w = uniformize<L>(group_broadcast<L>(ww, leader));
+    if (w < p.total) {
+      const int i = w / p.n_games;
+      g = w % p.n_games;
+      kind = uniformize<L>(p.kind[w]);
+      gr = genomes + (long)i * p.gstride;
+      load_net<L, U, O, WT>(nr, gr, H, b, lig);
+      if (kind == kOppNN) {
+        gl = opponents + (long)p.opp[w] * p.ostride;
+        load_net<L, U, O, WT>(nl, gl, H, b, lig);
+      }
+      st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
+      act_r = act_l = timeout = total = frames = 0;
+    }
+  };
+
+  start_game();
+  while (w < p.total) {
+    const int s1b = st.s1, s2b = st.s2;
+    const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
+    st.step(act_r, act_l);
+    frames += 1;
+    const int vis = st.vis;
+    const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
+    const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
+    int left = 0, right = 0;
+    if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
+      const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
+      if (kind == kOppNN) {
+        const int kl[6] = {320 - bx2, by2, 320 - lbx2, lby2, lc2, rc2};  // x flipped, main.py:146-147
+        left = decide<L, U, O, WT>(nl, gl, H, b, kl, lds, lig, slow);
+        c_fwd += 1;
+      } else if (kind == kOppScore) {
+        left = (st.s1 <= st.s2) ? hardcoded(by2, lc2) : 0;
+      } else {
+        left = hardcoded(by2, lc2);
+      }
+      const int kr[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
+      right = decide<L, U, O, WT>(nr, gr, H, b, kr, lds, lig, slow);
+      c_fwd += 1;
+    }
+    act_l = uniformize<L>(clamp_action(lc2, left));
+    act_r = uniformize<L>(clamp_action(rc2, right));
+    if (p.trace && w < p.trace_games && frames <= p.trace_cap && lig == 0)
+      p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+    if (frames > 1) {
+      if (st.s1 == s1b && st.s2 == s2b) {
+        timeout += 1;
+      } else {
+        total += timeout;
+        timeout = 0;
+      }
+    }
+    if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
+      if (lig == 0) finish_game(p, w, st, frames, total);
+      c_steps += frames;
+      c_games += 1;
+      start_game();
+    }
+  }
+  if (p.counters && lig == 0 && c_games) {
+    atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)c_steps);
+    atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
+    atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
+    atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
+  }
+}
+
+// ------------------------------------------------------------- fitness ----
+// evaluate()'s return: sum(all_rewards) (left to right from int 0) / float(GAMES_TO_PLAY).
+__global__ void k_fitness(const double *rewards, const int32_t *status_game, int n, int games,
+                          double *fitness, int32_t *status) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  int err = 0;
+  for (int g = 0; g < games; ++g) {
+    s = __dadd_rn(s, rewards[(long)i * games + g]);
+    err |= status_game[(long)i * games + g];
+  }
+  fitness[i] = s / (double)games;
+  if (status) status[i] = err;
+}
+
+// ============================================================ forward ====
+struct FwdParams {
+  const void *genomes;
+  const int32_t *gidx;
+  const double *x;
+  int32_t *index;
+  double *act;
+  uint64_t *counters;
+  int64_t gstride;
+  int n;
+  int nodes[PG_MAX_NODES];
+  int n_nodes, bias, max_width;
+};
+
+template <typename WT>
+__global__ __launch_bounds__(64) void k_forward_general(FwdParams p) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x;
+  const int W = p.max_width + 1;
+  const int n_in = p.nodes[0], n_out = p.nodes[p.n_nodes - 1];
+  for (int t = blockIdx.x; t < p.n; t += gridDim.x) {
+    const long row = p.gidx ? p.gidx[t] : t;
+    const WT *gw = (const WT *)p.genomes + row * p.gstride;
+    double *cur = lds, *nxt = lds + W;
+    for (int i = lane; i < n_in; i += 64) cur[i] = p.x[(long)t * n_in + i];
+    if (p.bias && lane == 0) cur[n_in] = 1.0;
+    wave_lds_sync();
+    const int idx = forward_f64_wave(gw, p.nodes, p.n_nodes, p.bias, cur, nxt, lane);
+    if (lane == 0) p.index[t] = idx;
+    if (p.act)
+      for (int j = lane; j < n_out; j += 64) p.act[(long)t * n_out + j] = cur[j];
+    wave_lds_sync();
+  }
+}
+
+template <int L, int U, int O, typename WT>
+__global__ __launch_bounds__(256) void k_forward_resident(FwdParams p) {
+  constexpr int GPB = 256 / L;
+  const int H = p.nodes[1], b = p.bias;
+  extern __shared__ double lds_all[];
+  const int lig = threadIdx.x & (L - 1);
+  const int grp = threadIdx.x / L;
+  double *lds = lds_all + grp * (H + 1 + O + 1);
+  uint32_t slow = 0;
+  for (int t = blockIdx.x * GPB + grp; t < p.n; t += gridDim.x * GPB) {
+    const long row = p.gidx ? p.gidx[t] : t;
+    const WT *gw = (const WT *)p.genomes + row * p.gstride;
+    Net<U, O> net;
+    load_net<L, U, O, WT>(net, gw, H, b, lig);
+    float x[6], z[O];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = (float)p.x[(long)t * 6 + i];
+    forward_f32<L, U, O>(net, x, z);
+    int idx = certify<O>(z, net.e);
+    if (idx >= 0 && p.act) {
+      // activations are reported within 2e-6: |S(z) - S(z_hat)| <= e * S'(max(|z_hat| - e, 0))
+      bool tight = true;
+#pragma unroll
+      for (int o = 0; o < O; ++o) {
+        const float t = fmaxf(fabsf(z[o]) - net.e[o], 0.f);
+        const float sp = __expf(-t) / ((1.f + __expf(-t)) * (1.f + __expf(-t)));
+        tight = tight && (net.e[o] * sp <= 2e-6f);
+      }
+      if (!tight) idx = -1;
+    }
+    if (idx < 0) {
+      double xd[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) xd[i] = p.x[(long)t * 6 + i];
+      idx = forward_f64_group<L, U, O, WT>(gw, H, b, xd, lds, lig);
+      if (p.act && lig < O) p.act[(long)t * O + lig] = lds[H + 1 + lig];
+      wave_lds_sync();
+      slow += (lig == 0);
+    } else if (p.act && lig < O) {
+      float zz = z[0];
+#pragma unroll
+      for (int o = 1; o < O; ++o) zz = (lig == o) ? z[o] : zz;
+      p.act[(long)t * O + lig] = sigmoid_f64((double)zz);
+    }
+    if (lig == 0) p.index[t] = idx;
+  }
+  if (p.counters && slow) atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
+}
+
+// ============================================================ physics ====
+__global__ void k_physics_reset(int32_t *s, int n, const uint64_t *seeds, const int32_t *one_player) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Pong st;
+  st.reset(seeds ? seeds[i] : 0ull, one_player ? one_player[i] : 0);
+  const int f[PG_STATE_FIELDS] = {st.bx, st.by, st.vx, st.vy, st.vis, st.timer, st.dir, st.hits,
+                                  st.point, st.lpy, st.rpy, st.s1, st.s2, st.one_player,
+                                  (int)(uint32_t)st.seed, (int)(uint32_t)(st.seed >> 32)};
+#pragma unroll
+  for (int k = 0; k < PG_STATE_FIELDS; ++k) s[(long)k * n + i] = f[k];
+}
+
+__global__ void k_physics_step(int32_t *s, int n, const uint8_t *actions) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Pong st;
+  st.bx = s[0L * n + i]; st.by = s[1L * n + i]; st.vx = s[2L * n + i]; st.vy = s[3L * n + i];
+  st.vis = s[4L * n + i]; st.timer = s[5L * n + i]; st.dir = s[6L * n + i]; st.hits = s[7L * n + i];
+  st.point = s[8L * n + i]; st.lpy = s[9L * n + i]; st.rpy = s[10L * n + i];
+  st.s1 = s[11L * n + i]; st.s2 = s[12L * n + i]; st.one_player = s[13L * n + i];
+  st.seed = (uint64_t)(uint32_t)s[14L * n + i] | ((uint64_t)(uint32_t)s[15L * n + i] << 32);
+  const int a = actions[i];
+  st.step(a & 3, (a >> 2) & 3);
+  s[0L * n + i] = st.bx; s[1L * n + i] = st.by; s[2L * n + i] = st.vx; s[3L * n + i] = st.vy;
+  s[4L * n + i] = st.vis; s[5L * n + i] = st.timer; s[6L * n + i] = st.dir; s[7L * n + i] = st.hits;
+  s[8L * n + i] = st.point; s[9L * n + i] = st.lpy; s[10L * n + i] = st.rpy;
+  s[11L * n + i] = st.s1; s[12L * n + i] = st.s2;
+}
+
+// ================================================================ GA =====
+// Counter-based uniform double in [0,1): splitmix64 of (seed, generation,
+// stream, a, b).  DEAP draws from Python's Mersenne Twister; the device GA
+// matches its distributions, not its stream (DESIGN.md "GA").
+__device__ __forceinline__ double u01(uint64_t seed, uint64_t gen, uint64_t stream, uint64_t a,
+                                      uint64_t b) {
+  uint64_t k = splitmix64(seed + 0x9E3779B97F4A7C15ull * (gen + 1));
+  k = splitmix64(k ^ (stream * 0xD6E8FEB86659FD93ull + a));
+  k = splitmix64(k ^ b);
+  return (double)(k >> 11) * 0x1.0p-53;
+}
+
+// tools.selTournament: for each pick, tournsize aspirants drawn with
+// replacement (selRandom = random.choice), the first maximum wins (max()).
+__global__ void k_select(pg_select_args a) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.k) return;
+  int best = -1;
+  double bf = 0.0;
+  for (int t = 0; t < a.tournsize; ++t) {
+    const int idx = (int)(u01(a.seed, a.generation, 1, (uint64_t)j, (uint64_t)t) * (double)a.n_pop);
+    const double f = a.fitness[idx];
+    if (best < 0 || f > bf) {
+      best = idx;
+      bf = f;
+    }
+  }
+  a.chosen[j] = best;
+}
+
+// selTournament by rank sampling (see pong_ga.h): P(winner rank <= r) = ((r+1)/n)^t.
+__global__ void k_select_ranked(pg_select_args a, const double *sorted, const int32_t *order) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.k) return;
+  const int n = a.n_pop;
+  const double v = u01(a.seed, a.generation, 8, (uint64_t)j, 0);
+  int r = (int)((double)n * exp(log(v) / (double)a.tournsize));
+  r = r < 0 ? 0 : (r > n - 1 ? n - 1 : r);
+  const double f = sorted[r];
+  int lo = 0, hi = n;  // tie group [first, last) of value f
+  int a0 = 0, b0 = r;
+  while (a0 < b0) { const int m = (a0 + b0) >> 1; if (sorted[m] < f) a0 = m + 1; else b0 = m; }
+  lo = a0;
+  a0 = r; b0 = n;
+  while (a0 < b0) { const int m = (a0 + b0) >> 1; if (sorted[m] <= f) a0 = m + 1; else b0 = m; }
+  hi = a0;
+  const int pick = lo + (int)(u01(a.seed, a.generation, 9, (uint64_t)j, 0) * (double)(hi - lo));
+  a.chosen[j] = order[pick < hi ? pick : hi - 1];
+}
+
+// algorithms.varAnd: clone the chosen parents, cxBlend consecutive pairs
+// (i-1, i) w.p. cxpb, then mutGaussian each individual w.p. mutpb.
+//   cxBlend:     gamma = (1 + 2 alpha) U - alpha; x1' = (1-gamma) x1 + gamma x2; x2' = gamma x1 + (1-gamma) x2
+//   mutGaussian: w.p. indpb per gene, x += N(mu, sigma)
+template <typename WT>
+__global__ void k_vary(pg_ga_args a) {
+  const long gene = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gene >= a.genes) return;
+  const WT *par = (const WT *)a.parents;
+  WT *off = (WT *)a.offspring;
+  const int pairs = (a.n + 1) / 2;
+  for (int pair = blockIdx.y; pair < pairs; pair += gridDim.y) {  // individuals 2*pair, 2*pair + 1
+    const int i0 = 2 * pair, i1 = 2 * pair + 1;
+    const bool has1 = i1 < a.n;
+    double x1 = (double)par[(long)a.chosen[i0] * a.stride + gene];
+    double x2 = has1 ? (double)par[(long)a.chosen[i1] * a.stride + gene] : 0.0;
+    const bool cx = has1 && u01(a.seed, a.generation, 2, (uint64_t)pair, 0) < a.cxpb;
+    if (cx) {
+      const double gamma =
+          __dadd_rn(__dmul_rn(1.0 + 2.0 * a.alpha, u01(a.seed, a.generation, 3, (uint64_t)pair, gene)), -a.alpha);
+      const double y1 = __dadd_rn(__dmul_rn(1.0 - gamma, x1), __dmul_rn(gamma, x2));
+      const double y2 = __dadd_rn(__dmul_rn(gamma, x1), __dmul_rn(1.0 - gamma, x2));
+      x1 = y1;
+      x2 = y2;
+    }
+    bool mut[2] = {false, false};
+    double xs[2] = {x1, x2};
+    for (int s = 0; s < (has1 ? 2 : 1); ++s) {
+      const int ind = i0 + s;
+      mut[s] = u01(a.seed, a.generation, 4, (uint64_t)ind, 0) < a.mutpb;
+      if (mut[s] && u01(a.seed, a.generation, 5, (uint64_t)ind, gene) < a.indpb) {
+        // Box-Muller from two counter-based uniforms
+        const double u1 = 1.0 - u01(a.seed, a.generation, 6, (uint64_t)ind, gene);
+        const double u2 = u01(a.seed, a.generation, 7, (uint64_t)ind, gene);
+        const double nrm = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        xs[s] = __dadd_rn(xs[s], __dadd_rn(a.mu, __dmul_rn(a.sigma, nrm)));
+      }
+    }
+    off[(long)i0 * a.stride + gene] = (WT)xs[0];
+    if (has1) off[(long)i1 * a.stride + gene] = (WT)xs[1];
+    if (gene == 0) {
+      a.invalid[i0] = (uint8_t)(cx || mut[0]);
+      if (has1) a.invalid[i1] = (uint8_t)(cx || mut[1]);
+    }
+  }
+}
+
+// ====================================================== host dispatch ====
+static int gene_count(const pg_net &n) {
+  const int b = n.bias ? 1 : 0;
+  long t = 0;
+  for (int i = 0; i + 1 < n.n_nodes; ++i) t += (long)(n.nodes[i] + b) * n.nodes[i + 1];
+  return t > 0x7fffffff ? -1 : (int)t;
+}
+
+static int32_t check_net(const pg_net &n, bool game) {
+  if (n.n_nodes < 2 || n.n_nodes > PG_MAX_NODES)
+    return fail(PG_ERR_INVALID, "net.n_nodes=%d must be in [2, %d]", n.n_nodes, PG_MAX_NODES);
+  for (int i = 0; i < n.n_nodes; ++i)
+    if (n.nodes[i] < 1 || n.nodes[i] > 65536)
+      return fail(PG_ERR_INVALID, "net.nodes[%d]=%d out of range", i, n.nodes[i]);
+  if (game && n.nodes[0] != 6)
+    return fail(PG_ERR_INVALID, "the game feeds 6 inputs (utils.py:146-152); nodes[0]=%d", n.nodes[0]);
+  if (n.dtype != PG_F32 && n.dtype != PG_F64) return fail(PG_ERR_INVALID, "net.dtype=%d", n.dtype);
+  if (gene_count(n) < 0) return fail(PG_ERR_INVALID, "network too large");
+  return PG_OK;
+}
+
+static int max_width(const pg_net &n) {
+  int m = 0;
+  for (int i = 0; i < n.n_nodes; ++i) m = n.nodes[i] > m ? n.nodes[i] : m;
+  return m;
+}
+
+static int g_num_cus = 0;
+static int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      g_num_cus = prop.multiProcessorCount;
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
+// Resident kernel table: (L, U) chosen from the hidden width H.
+struct ResidentChoice {
+  int L, U;
+};
+static ResidentChoice choose_resident(int H, int requested_L) {
+  static const ResidentChoice table[] = {{4, 1}, {8, 1}, {16, 1}, {32, 1}, {16, 4}, {32, 4}, {64, 4}};
+  static const ResidentChoice all[] = {{4, 1}, {8, 1}, {16, 1}, {32, 1}, {64, 1}, {16, 2}, {32, 2},
+                                       {64, 2}, {16, 4}, {32, 4}, {64, 4}};
+  if (requested_L > 0) {
+    for (const auto &c : all)
+      if (c.L == requested_L && c.L * c.U >= H) return c;
+    return {0, 0};
+  }
+  for (const auto &c : table)
+    if (c.L * c.U >= H) return c;
+  return {0, 0};
+}
+
+template <int L, int U, int O, typename WT>
+static int32_t launch_resident(const EvalParams &p, hipStream_t s) {
+  constexpr int GPB = 256 / L;
+  const size_t lds = (size_t)GPB * (p.nodes[1] + 1 + O + 1) * sizeof(double);
+  const int want = (p.total + GPB - 1) / GPB;
+  const int cap = num_cus() * 8;
+  const int grid = want < cap ? want : cap;
+  if (grid <= 0) return PG_OK;
+  hipLaunchKernelGGL((k_resident<L, U, O, WT>), dim3(grid), dim3(256), lds, s, p);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+template <int L, int U, typename WT>
+static int32_t launch_resident_o(const EvalParams &p, int O, hipStream_t s) {
+  switch (O) {
+    case 2: return launch_resident<L, U, 2, WT>(p, s);
+    case 3: return launch_resident<L, U, 3, WT>(p, s);
+    case 4: return launch_resident<L, U, 4, WT>(p, s);
+  }
+  return fail(PG_ERR_UNSUPPORTED, "resident kernel supports 2..4 outputs, got %d", O);
+}
+
+template <typename WT>
+static int32_t launch_resident_any(const EvalParams &p, ResidentChoice c, int O, hipStream_t s) {
+#define PG_RES(LL, UU) \
+  if (c.L == LL && c.U == UU) return launch_resident_o<LL, UU, WT>(p, O, s);
+  PG_RES(4, 1) PG_RES(8, 1) PG_RES(16, 1) PG_RES(32, 1) PG_RES(64, 1)
+  PG_RES(16, 2) PG_RES(32, 2) PG_RES(64, 2) PG_RES(16, 4) PG_RES(32, 4) PG_RES(64, 4)
+#undef PG_RES
+  return fail(PG_ERR_UNSUPPORTED, "no resident kernel for L=%d U=%d", c.L, c.U);
+}
+
+template <int L, int U, int O, typename WT>
+static int32_t launch_fwd_resident(const FwdParams &p, hipStream_t s) {
+  constexpr int GPB = 256 / L;
+  const size_t lds = (size_t)GPB * (p.nodes[1] + 1 + O + 1) * sizeof(double);
+  const int want = (p.n + GPB - 1) / GPB;
+  const int cap = num_cus() * 8;
+  const int grid = want < cap ? want : cap;
+  if (grid <= 0) return PG_OK;
+  hipLaunchKernelGGL((k_forward_resident<L, U, O, WT>), dim3(grid), dim3(256), lds, s, p);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+template <typename WT>
+static int32_t launch_fwd_resident_any(const FwdParams &p, ResidentChoice c, int O, hipStream_t s) {
+#define PG_FRES(LL, UU)                                                  \
+  if (c.L == LL && c.U == UU) {                                          \
+    if (O == 2) return launch_fwd_resident<LL, UU, 2, WT>(p, s);         \
+    if (O == 3) return launch_fwd_resident<LL, UU, 3, WT>(p, s);         \
+    if (O == 4) return launch_fwd_resident<LL, UU, 4, WT>(p, s);         \
+  }
+  PG_FRES(4, 1) PG_FRES(8, 1) PG_FRES(16, 1) PG_FRES(32, 1) PG_FRES(64, 1)
+  PG_FRES(16, 2) PG_FRES(32, 2) PG_FRES(64, 2) PG_FRES(16, 4) PG_FRES(32, 4) PG_FRES(64, 4)
+#undef PG_FRES
+  return fail(PG_ERR_UNSUPPORTED, "no resident forward kernel for L=%d U=%d O=%d", c.L, c.U, O);
+}
+
+static bool resident_shape_ok(const pg_net &n) {
+  return n.n_nodes == 3 && n.nodes[0] == 6 && n.nodes[1] <= 256 && n.nodes[2] >= 2 && n.nodes[2] <= 4;
+}
+
+}  // namespace pg
+
+using namespace pg;
+
+// ================================================================ C-ABI ===
+extern "C" {
+
+const char *pg_version(void) { return PG_VERSION_STRING; }
+int32_t pg_abi_version(void) { return PG_ABI_VERSION; }
+const char *pg_last_error(void) { return g_last_error.c_str(); }
+
+int32_t pg_device_count(void) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) return fail(PG_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  return n;
+}
+
+size_t pg_eval_workspace_bytes(const pg_eval_args *a) {
+  // [0, 256): dynamic game counter; then one int32 per game (zero-division flags)
+  const size_t games = a ? (size_t)(a->n_genomes > 0 ? a->n_genomes : 0) * (size_t)(a->n_games > 0 ? a->n_games : 0) : 0;
+  return 256 + ((games * sizeof(int32_t) + 255) / 256) * 256;
+}
+
+int32_t pg_gene_count(const pg_net *net) {
+  if (!net) return fail(PG_ERR_INVALID, "net is NULL");
+  int32_t rc = check_net(*net, false);
+  if (rc != PG_OK) return rc;
+  return gene_count(*net);
+}
+
+int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  int32_t rc = check_net(a->net, true);
+  if (rc != PG_OK) return rc;
+  if (a->n_genomes < 0) return fail(PG_ERR_INVALID, "n_genomes=%d < 0", a->n_genomes);
+  if (a->n_games < 1 || a->n_games > 64) return fail(PG_ERR_INVALID, "n_games=%d not in [1, 64]", a->n_games);
+  if (a->n_genomes == 0) return PG_OK;
+  const long total = (long)a->n_genomes * a->n_games;
+  if (total > 0x7fffffffL) return fail(PG_ERR_INVALID, "too many games (%ld)", total);
+  const int G = gene_count(a->net);
+  if (!a->genomes || a->genome_stride < G)
+    return fail(PG_ERR_INVALID, "genomes NULL or genome_stride=%lld < gene count %d", (long long)a->genome_stride, G);
+  if (!a->game_kind || !a->game_opp || !a->game_mult || !a->fitness || !a->rewards || !a->scores ||
+      !a->frames || !a->total_frames || !a->status)
+    return fail(PG_ERR_INVALID, "a required per-game array is NULL");
+  if (a->n_opponents > 0 && (!a->opponents || a->opponent_stride < G))
+    return fail(PG_ERR_INVALID, "opponents NULL or opponent_stride < gene count");
+  if (a->precision != PG_PREC_CERTIFIED && a->precision != PG_PREC_F64)
+    return fail(PG_ERR_INVALID, "precision=%d", a->precision);
+  if (a->trace && (a->trace_games < 0 || a->trace_cap < 1))
+    return fail(PG_ERR_INVALID, "trace needs trace_games >= 0 and trace_cap >= 1");
+  const size_t need = pg_eval_workspace_bytes(a);
+  if (!a->workspace || a->workspace_bytes < need)
+    return fail(PG_ERR_INVALID, "workspace of %zu bytes required (got %zu)", need, a->workspace_bytes);
+
+  hipStream_t s = (hipStream_t)stream;
+  EvalParams p;
+  memset(&p, 0, sizeof(p));
+  p.genomes = a->genomes;
+  p.opponents = a->opponents ? a->opponents : a->genomes;
+  p.kind = a->game_kind;
+  p.opp = a->game_opp;
+  p.mult = a->game_mult;
+  p.rewards = a->rewards;
+  p.scores = a->scores;
+  p.frames = a->frames;
+  p.total_frames = a->total_frames;
+  p.counters = a->counters;
+  p.trace = a->trace;
+  p.trace_games = a->trace ? a->trace_games : 0;
+  p.trace_cap = a->trace_cap;
+  p.work = (unsigned int *)a->workspace;
+  p.status_game = (int32_t *)((char *)a->workspace + 256);
+  p.gstride = a->genome_stride;
+  p.ostride = a->opponent_stride;
+  p.seed = a->seed;
+  p.n_genomes = a->n_genomes;
+  p.n_games = a->n_games;
+  p.total = (int)total;
+  for (int i = 0; i < a->net.n_nodes; ++i) p.nodes[i] = a->net.nodes[i];
+  p.n_nodes = a->net.n_nodes;
+  p.bias = a->net.bias ? 1 : 0;
+  p.max_width = max_width(a->net);
+
+  PG_HIP(hipMemsetAsync(a->workspace, 0, 256, s));
+  int kernel = a->kernel;
+  const bool res_ok = resident_shape_ok(a->net);
+  if (kernel == PG_KERNEL_AUTO) kernel = (res_ok && a->precision == PG_PREC_CERTIFIED) ? PG_KERNEL_RESIDENT : PG_KERNEL_GENERAL;
+  if (kernel == PG_KERNEL_RESIDENT) {
+    if (!res_ok) return fail(PG_ERR_UNSUPPORTED, "resident kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
+    if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "resident kernel is the certified-precision path");
+    const ResidentChoice c = choose_resident(a->net.nodes[1], a->group_lanes);
+    if (c.L == 0) return fail(PG_ERR_UNSUPPORTED, "no resident kernel for H=%d group_lanes=%d", a->net.nodes[1], a->group_lanes);
+    rc = a->net.dtype == PG_F64 ? launch_resident_any<double>(p, c, a->net.nodes[2], s)
+                                : launch_resident_any<float>(p, c, a->net.nodes[2], s);
+    if (rc != PG_OK) return rc;
+  } else if (kernel == PG_KERNEL_GENERAL) {
+    const size_t lds = 2 * (size_t)(p.max_width + 1) * sizeof(double);
+    if (lds > 160 * 1024) return fail(PG_ERR_UNSUPPORTED, "layer width %d too large for LDS", p.max_width);
+    const int cap = num_cus() * 16;
+    const int grid = total < cap ? (int)total : cap;
+    if (a->net.dtype == PG_F64)
+      hipLaunchKernelGGL(k_general<double>, dim3(grid), dim3(64), lds, s, p);
+    else
+      hipLaunchKernelGGL(k_general<float>, dim3(grid), dim3(64), lds, s, p);
+    PG_HIP(hipGetLastError());
+  } else {
+    return fail(PG_ERR_INVALID, "kernel=%d", a->kernel);
+  }
+  hipLaunchKernelGGL(k_fitness, dim3((a->n_genomes + 255) / 256), dim3(256), 0, s, a->rewards,
+                     p.status_game, a->n_genomes, a->n_games, a->fitness, a->status);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_forward(const pg_forward_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  int32_t rc = check_net(a->net, false);
+  if (rc != PG_OK) return rc;
+  if (a->n < 0) return fail(PG_ERR_INVALID, "n=%d < 0", a->n);
+  if (a->n == 0) return PG_OK;
+  const int G = gene_count(a->net);
+  if (!a->genomes || a->genome_stride < G || !a->x || !a->index)
+    return fail(PG_ERR_INVALID, "genomes/x/index NULL or genome_stride < gene count %d", G);
+  hipStream_t s = (hipStream_t)stream;
+  FwdParams p;
+  memset(&p, 0, sizeof(p));
+  p.genomes = a->genomes;
+  p.gidx = a->genome_index;
+  p.x = a->x;
+  p.index = a->index;
+  p.act = a->act;
+  p.counters = a->counters;
+  p.gstride = a->genome_stride;
+  p.n = a->n;
+  for (int i = 0; i < a->net.n_nodes; ++i) p.nodes[i] = a->net.nodes[i];
+  p.n_nodes = a->net.n_nodes;
+  p.bias = a->net.bias ? 1 : 0;
+  p.max_width = max_width(a->net);
+  if (a->precision == PG_PREC_CERTIFIED && resident_shape_ok(a->net)) {
+    const ResidentChoice c = choose_resident(a->net.nodes[1], 0);
+    return a->net.dtype == PG_F64 ? launch_fwd_resident_any<double>(p, c, a->net.nodes[2], s)
+                                  : launch_fwd_resident_any<float>(p, c, a->net.nodes[2], s);
+  }
+  if (a->precision != PG_PREC_CERTIFIED && a->precision != PG_PREC_F64)
+    return fail(PG_ERR_INVALID, "precision=%d", a->precision);
+  const size_t lds = 2 * (size_t)(p.max_width + 1) * sizeof(double);
+  if (lds > 160 * 1024) return fail(PG_ERR_UNSUPPORTED, "layer width %d too large for LDS", p.max_width);
+  const int cap = num_cus() * 16;
+  const int grid = a->n < cap ? a->n : cap;
+  if (a->net.dtype == PG_F64)
+    hipLaunchKernelGGL(k_forward_general<double>, dim3(grid), dim3(64), lds, s, p);
+  else
+    hipLaunchKernelGGL(k_forward_general<float>, dim3(grid), dim3(64), lds, s, p);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_physics_reset(int32_t *state, int32_t n, const uint64_t *seeds, const int32_t *one_player,
+                         void *stream) {
+  if (n < 0 || (n > 0 && !state)) return fail(PG_ERR_INVALID, "state NULL or n < 0");
+  if (n == 0) return PG_OK;
+  hipLaunchKernelGGL(k_physics_reset, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, state, n,
+                     seeds, one_player);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_physics_step(int32_t *state, int32_t n, const uint8_t *actions, void *stream) {
+  if (n < 0 || (n > 0 && (!state || !actions))) return fail(PG_ERR_INVALID, "state/actions NULL or n < 0");
+  if (n == 0) return PG_OK;
+  hipLaunchKernelGGL(k_physics_step, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, state, n,
+                     actions);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_ga_select_tournament(const pg_select_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  if (a->k < 0 || a->n_pop < 1 || a->tournsize < 1 || !a->fitness || !a->chosen)
+    return fail(PG_ERR_INVALID, "selTournament needs k >= 0, n_pop >= 1, tournsize >= 1 and buffers");
+  if (a->k == 0) return PG_OK;
+  hipLaunchKernelGGL(k_select, dim3((a->k + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_ga_select_tournament_ranked(const pg_select_args *a, const double *sorted_fitness,
+                                       const int32_t *order, void *stream) {
+  if (!a || !sorted_fitness || !order) return fail(PG_ERR_INVALID, "args/sorted_fitness/order is NULL");
+  if (a->k < 0 || a->n_pop < 1 || a->tournsize < 1 || !a->chosen)
+    return fail(PG_ERR_INVALID, "selTournament needs k >= 0, n_pop >= 1, tournsize >= 1 and buffers");
+  if (a->k == 0) return PG_OK;
+  hipLaunchKernelGGL(k_select_ranked, dim3((a->k + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a,
+                     sorted_fitness, order);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_ga_vary(const pg_ga_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  if (a->n < 0 || a->genes < 1 || a->stride < a->genes || !a->parents || !a->chosen || !a->offspring ||
+      !a->invalid || (a->dtype != PG_F32 && a->dtype != PG_F64))
+    return fail(PG_ERR_INVALID, "varAnd: bad sizes or NULL buffers");
+  if (a->n == 0) return PG_OK;
+  const int pairs = (a->n + 1) / 2;
+  dim3 grid((unsigned)((a->genes + 255) / 256), (unsigned)(pairs < 65535 ? pairs : 65535));
+  if (a->dtype == PG_F64)
+    hipLaunchKernelGGL(k_vary<double>, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  else
+    hipLaunchKernelGGL(k_vary<float>, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+}  // extern "C"

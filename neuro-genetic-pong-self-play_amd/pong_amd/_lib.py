@@ -1,0 +1,145 @@
+"""ctypes binding of ``libpong_ga.so`` (the C-ABI declared in ``include/pong_ga.h``).
+
+The structures below mirror the header field for field.  The library is the
+only compute path: if it is missing or cannot be loaded, :func:`lib` raises --
+there is no CPU fallback in the product.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_NAME = "libpong_ga.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
+
+PG_ABI_VERSION = 1
+PG_MAX_NODES = 9
+
+PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
+PG_F32, PG_F64 = 0, 1
+PG_OPP_HARDCODED, PG_OPP_ROM_CPU, PG_OPP_SCORE, PG_OPP_NN = 0, 1, 2, 3
+PG_PREC_CERTIFIED, PG_PREC_F64 = 0, 1
+PG_KERNEL_AUTO, PG_KERNEL_GENERAL, PG_KERNEL_RESIDENT = 0, 1, 2
+PG_STATE_FIELDS = 16
+STATE_FIELD_NAMES = ("ball_x", "ball_y", "ball_vx", "ball_vy", "ball_visible", "serve_timer",
+                     "serve_dir", "hits", "point", "lpy", "rpy", "score1", "score2",
+                     "one_player", "seed_lo", "seed_hi")
+
+_vp = ctypes.c_void_p
+
+
+class PgNet(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int32), ("nodes", ctypes.c_int32 * PG_MAX_NODES),
+                ("bias", ctypes.c_int32), ("dtype", ctypes.c_int32)]
+
+
+class PgEvalArgs(ctypes.Structure):
+    _fields_ = [
+        ("net", PgNet),
+        ("n_genomes", ctypes.c_int32), ("n_games", ctypes.c_int32),
+        ("genomes", _vp), ("genome_stride", ctypes.c_int64),
+        ("opponents", _vp), ("opponent_stride", ctypes.c_int64), ("n_opponents", ctypes.c_int32),
+        ("precision", ctypes.c_int32),
+        ("game_kind", _vp), ("game_opp", _vp), ("game_mult", _vp),
+        ("seed", ctypes.c_uint64),
+        ("fitness", _vp), ("rewards", _vp), ("scores", _vp), ("frames", _vp),
+        ("total_frames", _vp), ("status", _vp), ("counters", _vp),
+        ("trace", _vp), ("trace_games", ctypes.c_int32), ("trace_cap", ctypes.c_int32),
+        ("kernel", ctypes.c_int32), ("group_lanes", ctypes.c_int32),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class PgForwardArgs(ctypes.Structure):
+    _fields_ = [
+        ("net", PgNet), ("n", ctypes.c_int32), ("genomes", _vp), ("genome_stride", ctypes.c_int64),
+        ("genome_index", _vp), ("x", _vp), ("precision", ctypes.c_int32), ("index", _vp),
+        ("act", _vp), ("counters", _vp),
+    ]
+
+
+class PgGaArgs(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32), ("genes", ctypes.c_int64), ("dtype", ctypes.c_int32),
+        ("parents", _vp), ("stride", ctypes.c_int64), ("n_parents", ctypes.c_int32),
+        ("chosen", _vp), ("offspring", _vp), ("invalid", _vp),
+        ("cxpb", ctypes.c_double), ("mutpb", ctypes.c_double), ("alpha", ctypes.c_double),
+        ("mu", ctypes.c_double), ("sigma", ctypes.c_double), ("indpb", ctypes.c_double),
+        ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64),
+    ]
+
+
+class PgSelectArgs(ctypes.Structure):
+    _fields_ = [
+        ("n_pop", ctypes.c_int32), ("k", ctypes.c_int32), ("tournsize", ctypes.c_int32),
+        ("fitness", _vp), ("chosen", _vp), ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64),
+    ]
+
+
+# name -> (restype, argtypes); exactly the functions include/pong_ga.h declares
+SIGNATURES = {
+    "pg_version": (ctypes.c_char_p, []),
+    "pg_abi_version": (ctypes.c_int32, []),
+    "pg_last_error": (ctypes.c_char_p, []),
+    "pg_device_count": (ctypes.c_int32, []),
+    "pg_eval_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PgEvalArgs)]),
+    "pg_gene_count": (ctypes.c_int32, [ctypes.POINTER(PgNet)]),
+    "pg_eval_population": (ctypes.c_int32, [ctypes.POINTER(PgEvalArgs), _vp]),
+    "pg_forward": (ctypes.c_int32, [ctypes.POINTER(PgForwardArgs), _vp]),
+    "pg_physics_reset": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp, _vp]),
+    "pg_physics_step": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp]),
+    "pg_ga_select_tournament": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp]),
+    "pg_ga_select_tournament_ranked": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp, _vp, _vp]),
+    "pg_ga_vary": (ctypes.c_int32, [ctypes.POINTER(PgGaArgs), _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class PongGAError(RuntimeError):
+    """A libpong_ga call returned a negative pg_status."""
+
+    def __init__(self, func: str, code: int, message: str):
+        super().__init__(f"{func} failed ({code}): {message}")
+        self.code = code
+
+
+def lib() -> ctypes.CDLL:
+    """Load libpong_ga.so (built in-tree by ``pong_amd.build``); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            if L.pg_abi_version() != PG_ABI_VERSION:
+                raise RuntimeError(f"{LIB_PATH}: ABI {L.pg_abi_version()} != {PG_ABI_VERSION}")
+            _lib = L
+    return _lib
+
+
+def check(func: str, rc: int) -> None:
+    if rc != PG_OK:
+        msg = lib().pg_last_error()
+        raise PongGAError(func, rc, msg.decode() if msg else "")
+
+
+def make_net(nodes, bias=True, dtype=PG_F64) -> PgNet:
+    nodes = [int(n) for n in nodes]
+    if not 2 <= len(nodes) <= PG_MAX_NODES:
+        raise ValueError(f"NETWORK_SHAPE must have 2..{PG_MAX_NODES} entries, got {nodes}")
+    arr = (ctypes.c_int32 * PG_MAX_NODES)(*(nodes + [0] * (PG_MAX_NODES - len(nodes))))
+    return PgNet(len(nodes), arr, 1 if bias else 0, dtype)

@@ -1,0 +1,272 @@
+"""Device-resident entry points over ``libpong_ga.so``.
+
+PyTorch is used only to own device memory and streams: every compute call
+goes through the C-ABI (``include/pong_ga.h``) with ``data_ptr()`` pointers and
+the current HIP stream.  Nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+
+PRECISIONS = {"certified": L.PG_PREC_CERTIFIED, "f64": L.PG_PREC_F64}
+KERNELS = {"auto": L.PG_KERNEL_AUTO, "general": L.PG_KERNEL_GENERAL, "resident": L.PG_KERNEL_RESIDENT}
+DTYPES = {torch.float32: L.PG_F32, torch.float64: L.PG_F64}
+
+
+def gene_count(nodes, bias=True) -> int:
+    """utils.calculate_gene_size (utils.py:128-136) for an arbitrary shape."""
+    b = 1 if bias else 0
+    return sum((int(nodes[i]) + b) * int(nodes[i + 1]) for i in range(len(nodes) - 1))
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _need(t: torch.Tensor, name: str, dtype, device, shape=None):
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name} must live on {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+
+
+@dataclass
+class EvalResult:
+    """evaluate() outputs for a batch, all on the device."""
+
+    fitness: torch.Tensor       # [n] f64
+    rewards: torch.Tensor       # [n, games] f64
+    scores: torch.Tensor        # [n, games, 2] int32 (score1, score2)
+    frames: torch.Tensor        # [n, games] int32 env steps
+    total_frames: torch.Tensor  # [n, games] f64
+    status: torch.Tensor        # [n] int32, 1 = ZeroDivisionError
+    counters: torch.Tensor      # [4] int64: env steps, NN forwards, f64 re-decisions, games
+
+
+class Evaluator:
+    """Population evaluator for one NETWORK_SHAPE on one device."""
+
+    def __init__(self, nodes, bias=True, dtype=torch.float64, device=None, n_games=6,
+                 precision="certified", kernel="auto", group_lanes=0, seed=0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("pong_amd.Evaluator needs a HIP device (no CPU fallback)")
+        L.lib()
+        self.nodes = [int(n) for n in nodes]
+        self.bias = bool(bias)
+        self.dtype = dtype
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.n_games = int(n_games)
+        self.precision = precision
+        self.kernel = kernel
+        self.group_lanes = int(group_lanes)
+        self.seed = int(seed)
+        self.genes = gene_count(self.nodes, self.bias)
+        self.net = L.make_net(self.nodes, self.bias, DTYPES[dtype])
+        self._ws = None
+
+    # ------------------------------------------------------------ schedules
+    def selfplay_schedule(self, n: int, n_opponents: int, offset: int = 0):
+        """All games NN vs hall-of-fame row (global_index * games + g) % n_opponents."""
+        dev = self.device
+        gi = (torch.arange(n, device=dev, dtype=torch.int64) + offset)[:, None] * self.n_games
+        gi = gi + torch.arange(self.n_games, device=dev, dtype=torch.int64)[None, :]
+        kind = torch.full((n, self.n_games), L.PG_OPP_NN, dtype=torch.int32, device=dev)
+        opp = (gi % max(n_opponents, 1)).to(torch.int32)
+        mult = torch.ones((n, self.n_games), dtype=torch.float64, device=dev)
+        return kind, opp, mult
+
+    # ------------------------------------------------------------- evaluate
+    def _workspace(self, args: L.PgEvalArgs) -> torch.Tensor:
+        need = L.lib().pg_eval_workspace_bytes(ctypes.byref(args))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 4096), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def evaluate(self, genomes: torch.Tensor, kind: torch.Tensor, opp: torch.Tensor, mult: torch.Tensor,
+                 opponents: Optional[torch.Tensor] = None, trace_games: int = 0, trace_cap: int = 0,
+                 out: Optional[EvalResult] = None, precision: Optional[str] = None,
+                 kernel: Optional[str] = None, group_lanes: Optional[int] = None, validate: bool = True):
+        """Run every genome's games to termination; returns (EvalResult, trace or None).
+
+        ``validate`` checks the schedule's opponent rows on the host first (one
+        device sync); callers that built the schedule themselves may skip it.
+        """
+        dev = self.device
+        n = genomes.shape[0]
+        games = self.n_games
+        _need(genomes, "genomes", self.dtype, dev)
+        if genomes.dim() != 2 or genomes.shape[1] < self.genes:
+            raise ValueError(f"genomes must be [n, >= {self.genes}], got {tuple(genomes.shape)}")
+        _need(kind, "kind", torch.int32, dev, (n, games))
+        _need(opp, "opp", torch.int32, dev, (n, games))
+        _need(mult, "mult", torch.float64, dev, (n, games))
+        if opponents is not None:
+            _need(opponents, "opponents", self.dtype, dev)
+            if opponents.dim() != 2 or opponents.shape[1] < self.genes:
+                raise ValueError(f"opponents must be [H, >= {self.genes}], got {tuple(opponents.shape)}")
+        if validate and n:
+            # one host sync: out-of-range rows would fault the GPU, so check before launching
+            nn_games = kind == L.PG_OPP_NN
+            if bool(((kind < 0) | (kind > L.PG_OPP_NN)).any()):
+                raise ValueError("kind values must be pg_opp_kind codes 0..3")
+            if bool(nn_games.any()):
+                h = 0 if opponents is None else opponents.shape[0]
+                bad = nn_games & ((opp < 0) | (opp >= h))
+                if bool(bad.any()):
+                    raise ValueError(f"opp rows must index the {h}-row opponents tensor")
+        if out is None:
+            out = EvalResult(
+                fitness=torch.empty(n, dtype=torch.float64, device=dev),
+                rewards=torch.empty((n, games), dtype=torch.float64, device=dev),
+                scores=torch.empty((n, games, 2), dtype=torch.int32, device=dev),
+                frames=torch.empty((n, games), dtype=torch.int32, device=dev),
+                total_frames=torch.empty((n, games), dtype=torch.float64, device=dev),
+                status=torch.empty(n, dtype=torch.int32, device=dev),
+                counters=torch.zeros(4, dtype=torch.int64, device=dev))
+        else:
+            out.counters.zero_()
+        trace = None
+        if trace_games and trace_cap:
+            trace = torch.zeros((trace_games, trace_cap), dtype=torch.uint8, device=dev)
+        a = L.PgEvalArgs()
+        a.net = self.net
+        a.n_genomes = n
+        a.n_games = games
+        a.genomes = _ptr(genomes)
+        a.genome_stride = genomes.stride(0) if n > 1 else genomes.shape[1]
+        if opponents is not None and opponents.shape[0] > 0:
+            a.opponents = _ptr(opponents)
+            a.opponent_stride = opponents.stride(0) if opponents.shape[0] > 1 else opponents.shape[1]
+            a.n_opponents = opponents.shape[0]
+        a.precision = PRECISIONS[precision or self.precision]
+        a.game_kind, a.game_opp, a.game_mult = _ptr(kind), _ptr(opp), _ptr(mult)
+        a.seed = self.seed
+        a.fitness, a.rewards, a.scores = _ptr(out.fitness), _ptr(out.rewards), _ptr(out.scores)
+        a.frames, a.total_frames, a.status = _ptr(out.frames), _ptr(out.total_frames), _ptr(out.status)
+        a.counters = _ptr(out.counters)
+        if trace is not None:
+            a.trace, a.trace_games, a.trace_cap = _ptr(trace), trace_games, trace_cap
+        a.kernel = KERNELS[kernel or self.kernel]
+        a.group_lanes = self.group_lanes if group_lanes is None else int(group_lanes)
+        ws = self._workspace(a)
+        a.workspace, a.workspace_bytes = _ptr(ws), ws.numel()
+        with torch.cuda.device(dev):
+            L.check("pg_eval_population", L.lib().pg_eval_population(ctypes.byref(a), _stream(dev)))
+        return out, trace
+
+    # -------------------------------------------------------------- forward
+    def forward(self, genomes: torch.Tensor, x: torch.Tensor, genome_index: Optional[torch.Tensor] = None,
+                precision: Optional[str] = None, want_act: bool = True):
+        """Batched NeuralNetwork.run: returns (argmax index [n] int32, activations [n, out] f64)."""
+        dev = self.device
+        _need(genomes, "genomes", self.dtype, dev)
+        n = x.shape[0]
+        _need(x, "x", torch.float64, dev, (n, self.nodes[0]))
+        if genome_index is not None:
+            _need(genome_index, "genome_index", torch.int32, dev, (n,))
+        index = torch.empty(n, dtype=torch.int32, device=dev)
+        act = torch.empty((n, self.nodes[-1]), dtype=torch.float64, device=dev) if want_act else None
+        counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        a = L.PgForwardArgs()
+        a.net = self.net
+        a.n = n
+        a.genomes = _ptr(genomes)
+        a.genome_stride = genomes.stride(0) if genomes.shape[0] > 1 else genomes.shape[1]
+        a.genome_index = _ptr(genome_index)
+        a.x = _ptr(x)
+        a.precision = PRECISIONS[precision or self.precision]
+        a.index = _ptr(index)
+        a.act = _ptr(act)
+        a.counters = _ptr(counters)
+        with torch.cuda.device(dev):
+            L.check("pg_forward", L.lib().pg_forward(ctypes.byref(a), _stream(dev)))
+        self.last_forward_counters = counters
+        return index, act
+
+
+class Physics:
+    """The SoA Pong stepper (pg_physics_reset / pg_physics_step) for n games."""
+
+    def __init__(self, n: int, device=None):
+        L.lib()
+        self.n = int(n)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.state = torch.zeros((L.PG_STATE_FIELDS, self.n), dtype=torch.int32, device=self.device)
+
+    def reset(self, seeds: torch.Tensor, one_player: Optional[torch.Tensor] = None):
+        _need(seeds, "seeds", torch.int64, self.device, (self.n,))
+        if one_player is not None:
+            _need(one_player, "one_player", torch.int32, self.device, (self.n,))
+        with torch.cuda.device(self.device):
+            L.check("pg_physics_reset", L.lib().pg_physics_reset(
+                _ptr(self.state), self.n, _ptr(seeds), _ptr(one_player), _stream(self.device)))
+
+    def step(self, actions: torch.Tensor):
+        """actions [n] uint8: bit0 right up, bit1 right down, bit2 left up, bit3 left down."""
+        _need(actions, "actions", torch.uint8, self.device, (self.n,))
+        with torch.cuda.device(self.device):
+            L.check("pg_physics_step", L.lib().pg_physics_step(
+                _ptr(self.state), self.n, _ptr(actions), _stream(self.device)))
+
+    def fields(self) -> dict:
+        s = self.state.cpu()
+        return {name: s[i] for i, name in enumerate(L.STATE_FIELD_NAMES)}
+
+
+def select_tournament(fitness: torch.Tensor, k: int, tournsize: int, seed: int, generation: int) -> torch.Tensor:
+    """tools.selTournament on device: returns [k] int32 rows of the winners."""
+    _need(fitness, "fitness", torch.float64, fitness.device)
+    chosen = torch.empty(k, dtype=torch.int32, device=fitness.device)
+    a = L.PgSelectArgs(fitness.shape[0], k, tournsize, _ptr(fitness), _ptr(chosen), seed, generation)
+    with torch.cuda.device(fitness.device):
+        L.check("pg_ga_select_tournament", L.lib().pg_ga_select_tournament(ctypes.byref(a), _stream(fitness.device)))
+    return chosen
+
+
+def select_tournament_ranked(fitness: torch.Tensor, k: int, tournsize: int, seed: int, generation: int) -> torch.Tensor:
+    """tools.selTournament's winner distribution by rank sampling (O(n log n), any tournsize)."""
+    _need(fitness, "fitness", torch.float64, fitness.device)
+    sorted_fit, order = torch.sort(fitness, stable=True)
+    order = order.to(torch.int32)
+    chosen = torch.empty(k, dtype=torch.int32, device=fitness.device)
+    a = L.PgSelectArgs(fitness.shape[0], k, tournsize, _ptr(fitness), _ptr(chosen), seed, generation)
+    with torch.cuda.device(fitness.device):
+        L.check("pg_ga_select_tournament_ranked", L.lib().pg_ga_select_tournament_ranked(
+            ctypes.byref(a), _ptr(sorted_fit), _ptr(order), _stream(fitness.device)))
+    return chosen
+
+
+def vary(parents: torch.Tensor, chosen: torch.Tensor, genes: int, cxpb: float, mutpb: float, alpha: float,
+         mu: float, sigma: float, indpb: float, seed: int, generation: int, out: Optional[torch.Tensor] = None):
+    """algorithms.varAnd(cxBlend, mutGaussian) on device: returns (offspring, invalid[n] uint8)."""
+    dev = parents.device
+    n = chosen.shape[0]
+    _need(chosen, "chosen", torch.int32, dev, (n,))
+    if out is None:
+        out = torch.empty((n, parents.shape[1]), dtype=parents.dtype, device=dev)
+    invalid = torch.empty(n, dtype=torch.uint8, device=dev)
+    a = L.PgGaArgs()
+    a.n, a.genes, a.dtype = n, genes, DTYPES[parents.dtype]
+    a.parents, a.stride, a.n_parents = _ptr(parents), parents.stride(0), parents.shape[0]
+    a.chosen, a.offspring, a.invalid = _ptr(chosen), _ptr(out), _ptr(invalid)
+    a.cxpb, a.mutpb, a.alpha, a.mu, a.sigma, a.indpb = cxpb, mutpb, alpha, mu, sigma, indpb
+    a.seed, a.generation = seed, generation
+    if out.stride(0) != parents.stride(0):
+        raise ValueError("offspring and parents must share the row stride")
+    with torch.cuda.device(dev):
+        L.check("pg_ga_vary", L.lib().pg_ga_vary(ctypes.byref(a), _stream(dev)))
+    return out, invalid

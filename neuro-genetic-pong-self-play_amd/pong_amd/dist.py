@@ -1,0 +1,53 @@
+"""Population sharding over ranks and the one collective of a generation.
+
+The reference farms individuals out to SCOOP workers (ga.py:83
+``futures.map``).  Here rank r of N evaluates the contiguous rows
+``shard_range(P, r, N)`` of a replicated population, and the fitness vector is
+all-gathered once per generation (RCCL over xGMI with the "nccl" backend on
+MI355X; gloo in the CPU tests).  Nothing else crosses ranks: the GA state is
+replicated and updated identically from the same counter-based RNG keys.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Rows [lo, hi) of rank ``rank``: contiguous, sizes differ by at most one."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    base, rem = divmod(int(n), int(world))
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def gather_fitness(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
+    """All-gather each rank's fitness shard into the full [n_total] vector, in row order."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_range(n_total, rank, world)
+    if local.shape[0] != hi - lo:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} fitness values, expected {hi - lo}")
+    width = -(-n_total // world)  # ceil: all_gather needs equal sizes
+    buf = torch.zeros(width, dtype=local.dtype, device=local.device)
+    buf[: hi - lo] = local
+    out = torch.empty(width * world, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    parts = []
+    for r in range(world):
+        a, b = shard_range(n_total, r, world)
+        parts.append(out[r * width: r * width + (b - a)])
+    return torch.cat(parts)
+
+
+def evaluate_sharded(evaluate_rows, n_total: int, group=None):
+    """Evaluate this rank's rows with ``evaluate_rows(lo, hi) -> fitness tensor``
+    and return the full fitness vector on every rank."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    lo, hi = shard_range(n_total, rank, world)
+    local = evaluate_rows(lo, hi)
+    if world == 1:
+        return local
+    return gather_fitness(local, n_total, group)
