@@ -168,8 +168,14 @@ __device__ __forceinline__ float group_sum(float v) {
   if constexpr (L >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
   if constexpr (L >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror: quad <-> quad
   if constexpr (L >= 16) v += dpp_mov<0x140>(v); // row_mirror: half-row <-> half-row
-  if constexpr (L >= 32) v += __shfl_xor(v, 16, 64);
-  if constexpr (L >= 64) v += __shfl_xor(v, 32, 64);
+  if constexpr (L >= 32) {  // rows 0<->1, 2<->3: v_permlane16_swap (gfx950)
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  if constexpr (L >= 64) {  // half-waves 0-31 <-> 32-63: v_permlane32_swap (gfx950)
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
   return v;
 }
 

@@ -27,6 +27,7 @@
 
 #include "../../include/pong_ga.h"
 #include "pg_device.hpp"
+#include "pg_f64math.h"
 
 #ifndef PG_VERSION_STRING
 #define PG_VERSION_STRING "pong_ga 0.1.0 (gfx950)"
@@ -225,6 +226,18 @@ __global__ __launch_bounds__(64) void k_general(EvalParams p) {
 }
 
 // ================================================== resident (fast) path ==
+#ifndef PG_SLOW_INLINE
+#define PG_SLOW_INLINE __forceinline__
+#endif
+// minimum waves per SIMD requested from the register allocator (0 = no request)
+#ifndef PG_RES_WAVES
+#define PG_RES_WAVES 0
+#endif
+#if PG_RES_WAVES > 0
+#define PG_RES_BOUNDS __launch_bounds__(256, PG_RES_WAVES)
+#else
+#define PG_RES_BOUNDS __launch_bounds__(256)
+#endif
 constexpr float kU = 5.9604644775390625e-8f;  // 2^-24, f32 unit roundoff
 
 template <int U, int O>
@@ -232,18 +245,18 @@ struct Net {
   float w1[U][7];  // hidden unit j = lane + L*u: 6 input weights + bias weight
   float w2[U][O];  // output weights of that hidden unit
   float c[O];      // output biases
-  float e[O];      // certified error bound of each output pre-activation
+  float e;         // certified bound on |z_o(f32) - z_o(exact)|, max over outputs
 };
 
 // Loads the [6, H, O] genome's weights for this lane (numpy_nn.py:52-69
 // layout: layer l is a row-major (out, in + bias) block, bias column last) and
-// computes the error bound E_o of the f32 output pre-activations:
+// computes the error bound of the f32 output pre-activations:
 //   hidden a_j error  <= 11u R_j           (R_j = sum_i |W1_ji| incl. bias; |x_i| <= 1)
 //   sigmoid error     <= 2.75u R_j + 4.5u  (v_exp_f32/v_rcp_f32 ~1 ulp, slope <= 1/4)
 //   output z_o error  <= sum_j |W2_oj| (3u R_j + 5u) + 13u (sum_j |W2_oj| + |c_o|)
-// and keeps twice that (DESIGN.md "Certified argmax").
+// and keeps twice the largest over o (DESIGN.md "Certified argmax").
 template <int L, int U, int O, typename WT>
-__device__ void load_net(Net<U, O> &n, const WT *__restrict__ g, int H, int b, int lig) {
+__device__ __forceinline__ void load_net(Net<U, O> &n, const WT *__restrict__ g, int H, int b, int lig) {
   const int cols = 6 + b;
   const long off2 = (long)H * cols;
   float acc[O];
@@ -253,24 +266,30 @@ __device__ void load_net(Net<U, O> &n, const WT *__restrict__ g, int H, int b, i
   for (int u = 0; u < U; ++u) {
     const int j = lig + L * u;
     const bool ok = j < H;
+    const int jj = ok ? j : 0;  // padding units load a valid row and are zeroed
     float r = 0.f;
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
-      const bool use = ok && (i < 6 || b);
-      n.w1[u][i] = use ? (float)g[(long)j * cols + i] : 0.f;
+      const int ii = (i < 6 || b) ? i : 0;
+      const float v = (float)g[(long)jj * cols + ii];
+      n.w1[u][i] = (ok && (i < 6 || b)) ? v : 0.f;
       r += fabsf(n.w1[u][i]);
     }
 #pragma unroll
     for (int o = 0; o < O; ++o) {
-      n.w2[u][o] = ok ? (float)g[off2 + (long)o * (H + b) + j] : 0.f;
+      const float v = (float)g[off2 + (long)o * (H + b) + jj];
+      n.w2[u][o] = ok ? v : 0.f;
       acc[o] += fabsf(n.w2[u][o]) * (3.f * r + 18.f);
     }
   }
+  float e = 0.f;
 #pragma unroll
   for (int o = 0; o < O; ++o) {
-    n.c[o] = b ? (float)g[off2 + (long)o * (H + b) + H] : 0.f;
-    n.e[o] = 2.f * kU * (group_sum<L>(acc[o]) + 13.f * fabsf(n.c[o]));
+    const float v = (float)g[off2 + (long)o * (H + b) + (b ? H : 0)];
+    n.c[o] = b ? v : 0.f;
+    e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + 13.f * fabsf(n.c[o])));
   }
+  n.e = e;
 }
 
 __device__ __forceinline__ float sigmoid_f32(float a) {
@@ -278,9 +297,9 @@ __device__ __forceinline__ float sigmoid_f32(float a) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a * -1.4426950408889634f));
 }
 
-template <int L, int U, int O>
-__device__ __forceinline__ void forward_f32(const Net<U, O> &n, const float x[6], float z[O]) {
-  float acc[O];
+// Hidden layer and the lane-partial output sums of one network for this lane.
+template <int U, int O>
+__device__ __forceinline__ void partial_f32(const Net<U, O> &n, const float x[6], float acc[O]) {
 #pragma unroll
   for (int o = 0; o < O; ++o) acc[o] = 0.f;
 #pragma unroll
@@ -292,87 +311,157 @@ __device__ __forceinline__ void forward_f32(const Net<U, O> &n, const float x[6]
 #pragma unroll
     for (int o = 0; o < O; ++o) acc[o] = fmaf(n.w2[u][o], s, acc[o]);
   }
-#pragma unroll
-  for (int o = 0; o < O; ++o) z[o] = group_sum<L>(acc[o]) + n.c[o];
 }
 
 // Certified argmax of S(z) = 1/(1 + pow(e, -z)) in f64 (numpy_nn.py:22-23,131)
-// given |z_true - z[o]| <= e[o].  S is exactly 1.0 iff z >= 53 ln 2 =
+// given |z_true - z[o]| <= e.  S is exactly 1.0 iff z >= 53 ln 2 =
 // 36.73680056967710 (then every saturated output ties and the first wins);
-// below that, S rounds onto plateaus whose width in z is at most
-// 2^-52 (e^z + 1) (x4 margin below).  Returns -1 when the bound cannot prove
-// the f64 decision; the caller then recomputes the forward pass in f64.
+// below that S rounds onto plateaus no wider than 2^-52 (e^z + 1) in z (x4
+// margin below).  Returns -1 when the bound cannot prove the f64 decision;
+// the caller then recomputes the forward pass in f64.
 template <int O>
-__device__ __forceinline__ int certify(const float z[O], const float e[O]) {
+__device__ __forceinline__ int certify_general(const float z[O], float e) {
+  int res = -2;  // -2: undecided yet
 #pragma unroll
   for (int o = 0; o < O; ++o) {
-    if (!(z[o] + e[o] < 36.7367f)) return (z[o] - e[o] > 36.7369f) ? o : -1;
+    if (res == -2 && !(z[o] + e < 36.7367f)) res = (z[o] - e > 36.7369f) ? o : -1;
   }
+  if (res != -2) return res;
   int w = 0;
+  float zw = z[0];
 #pragma unroll
-  for (int o = 1; o < O; ++o)
-    if (z[o] > z[w]) w = o;
-  const float lo = z[w] - e[w];
-  const float tw = 8.8817842e-16f * (__expf(z[w] + e[w]) + 1.0f);
+  for (int o = 1; o < O; ++o) {
+    const bool gt = z[o] > zw;
+    w = gt ? o : w;
+    zw = gt ? z[o] : zw;
+  }
+  const float lo = zw - e;
+  const float tw = 8.8817842e-16f * (__expf(zw + e) + 1.0f);
   bool ok = true;
 #pragma unroll
-  for (int k = 0; k < O; ++k)
-    if (k != w) ok = ok && (lo - (z[k] + e[k]) > tw);
+  for (int k = 0; k < O; ++k) ok = ok && (k == w || lo - (z[k] + e) > tw);
   return ok ? w : -1;
+}
+
+template <int O>
+__device__ __forceinline__ int certify(const float z[O], float e) {
+  // common case: every output far below saturation (top + e < 20, where the
+  // plateau width is < 4.4e-7); the winner must lead the runner-up by 2e + that.
+  float top1, top2;
+  int w;
+  if constexpr (O == 2) {
+    w = z[1] > z[0] ? 1 : 0;
+    top1 = fmaxf(z[0], z[1]);
+    top2 = fminf(z[0], z[1]);
+  } else if constexpr (O == 3) {
+    top1 = fmaxf(fmaxf(z[0], z[1]), z[2]);
+    top2 = __builtin_amdgcn_fmed3f(z[0], z[1], z[2]);
+    w = (z[0] == top1) ? 0 : ((z[1] == top1) ? 1 : 2);
+  } else {
+    w = 0;
+    top1 = z[0];
+    top2 = -3.0e38f;
+#pragma unroll
+    for (int o = 1; o < O; ++o) {
+      const bool gt = z[o] > top1;
+      top2 = gt ? top1 : fmaxf(top2, z[o]);
+      w = gt ? o : w;
+      top1 = gt ? z[o] : top1;
+    }
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int o = 0; o < O; ++o) sum += z[o];
+  if (sum == sum && top1 + e < 20.0f) return (top1 - top2 > 2.f * e + 4.4e-7f) ? w : -1;
+  return certify_general<O>(z, e);
 }
 
 // The f64 re-decision of one forward pass by the L lanes of a group, in
 // numpy_nn's order (sequential dot products), hidden activations in LDS.
-// Returns the argmax; writes the output activations to act (group LDS) too.
+// Returns the argmax; leaves the output activations in lds[H+1 ..].
 template <int L, int U, int O, typename WT>
-__device__ int forward_f64_group(const WT *__restrict__ g, int H, int b, const double x[6], double *lds,
-                                 int lig) {
+__device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H, int b, const int *k, double *lds,
+                                              int lig) {
+  double x[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
   const int cols = 6 + b;
+#pragma unroll 1
+  for (int j = lig; j < H; j += L) {
+    const WT *row = g + (long)j * cols;
+    double z = 0.0;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int j = lig + L * u;
-    if (j < H) {
-      const WT *row = g + (long)j * cols;
-      double z = 0.0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], x[i]));
-      if (b) z = __dadd_rn(z, (double)row[6]);
-      lds[j] = sigmoid_f64(z);
-    }
+    for (int i = 0; i < 6; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], x[i]));
+    if (b) z = __dadd_rn(z, (double)row[6]);
+    lds[j] = pg_sigmoid_f64(z);
   }
   wave_lds_sync();
   if (lig < O) {
     const WT *v = g + (long)H * cols + (long)lig * (H + b);
     double z = 0.0;
+#pragma unroll 1
     for (int j = 0; j < H; ++j) z = __dadd_rn(z, __dmul_rn((double)v[j], lds[j]));
     if (b) z = __dadd_rn(z, (double)v[H]);
-    lds[H + 1 + lig] = sigmoid_f64(z);
+    lds[H + 1 + lig] = pg_sigmoid_f64(z);
   }
   wave_lds_sync();
   int best = 0;
-#pragma unroll
   for (int o = 1; o < O; ++o)
     if (lds[H + 1 + o] > lds[H + 1 + best]) best = o;
+  wave_lds_sync();
   return best;
 }
 
+__device__ __forceinline__ float feat32(int k) { return (float)k * 0.003125f; }  // k / 320, <= 2u rel. error
+
+// One frame's decisions: the right paddle's network always, the left paddle's
+// when it is a network too (self-play / hall-of-fame games).  The two f32
+// passes are independent, so their hidden layers and reductions interleave.
+// Any undecided argmax is re-decided by ONE f64 code site (keeps the rare
+// path's registers and code out of the hot loop's way).
 template <int L, int U, int O, typename WT>
-__device__ __forceinline__ int decide(const Net<U, O> &n, const WT *g, int H, int b, const int k[6],
-                                      double *lds, int lig, uint32_t &slow) {
-  float x[6], z[O];
+__device__ __forceinline__ void decide(Net<U, O> &nr, const WT *gr, const int kr[6], Net<U, O> &nl,
+                                       const WT *gl, const int kl[6], bool left_nn, int H, int b, double *lds,
+                                       int lig, uint32_t &slow, int &right, int &left) {
+  float xr[6], ar[O], zr[O];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) x[i] = (float)k[i] * 0.003125f;  // k / 320, <= 2u relative error
-  forward_f32<L, U, O>(n, x, z);
-  int idx = certify<O>(z, n.e);
-  if (idx < 0) {  // group-uniform: every lane of the group holds the same z
-    double xd[6];
+  for (int i = 0; i < 6; ++i) xr[i] = feat32(kr[i]);
+  partial_f32<U, O>(nr, xr, ar);
+  int il = 0;
+  if (left_nn) {
+    float xl[6], al[O], zl[O];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) xd[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
-    idx = forward_f64_group<L, U, O, WT>(g, H, b, xd, lds, lig);
-    wave_lds_sync();
-    slow += 1;
+    for (int i = 0; i < 6; ++i) xl[i] = feat32(kl[i]);
+    partial_f32<U, O>(nl, xl, al);
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      zr[o] = group_sum<L>(ar[o]) + nr.c[o];
+      zl[o] = group_sum<L>(al[o]) + nl.c[o];
+    }
+    il = certify<O>(zl, nl.e);
+  } else {
+#pragma unroll
+    for (int o = 0; o < O; ++o) zr[o] = group_sum<L>(ar[o]) + nr.c[o];
   }
-  return index_to_code(idx);
+  int ir = certify<O>(zr, nr.e);
+  if (ir < 0 || il < 0) {  // rare and group-uniform
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {
+      if ((side == 0 ? ir : il) >= 0) continue;
+      int k[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) k[i] = side ? kl[i] : kr[i];
+      const int idx = forward_f64_group<L, U, O, WT>(side ? gl : gr, H, b, k, lds, lig);
+      if (side) il = idx; else ir = idx;
+      slow += 1;
+    }
+    // Re-read the weights instead of keeping them live across the f64 pass:
+    // the rare path then does not add its registers to the hot loop's budget.
+    load_net<L, U, O, WT>(nr, gr, H, b, lig);
+    if (left_nn) load_net<L, U, O, WT>(nl, gl, H, b, lig);
+  }
+  right = index_to_code(ir);
+  if (left_nn) left = index_to_code(il);
 }
 
 template <int L>
@@ -382,8 +471,7 @@ __device__ __forceinline__ int group_broadcast(int v, int leader_lane) {
 }
 
 template <int L, int U, int O, typename WT>
-__global__ __launch_bounds__(256) void k_resident(EvalParams p) {
-  constexpr int GPB = 256 / L;  // game groups per block
+__global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
   const int H = p.nodes[1];
   const int b = p.bias;
   extern __shared__ double lds_all[];
@@ -397,18 +485,22 @@ __global__ __launch_bounds__(256) void k_resident(EvalParams p) {
 
   Net<U, O> nr, nl;
   Pong st;
-  int w = 0, kind = 0, g = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
-  const WT *gr = nullptr, *gl = nullptr;
+  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
+  const WT *gr = genomes, *gl = genomes;
   uint32_t slow = 0, c_fwd = 0;
   uint64_t c_steps = 0, c_games = 0;
 
-  auto start_game = [&]() {
+  int w;
+  {
     int ww = 0;
     if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
     w = uniformize<L>(group_broadcast<L>(ww, leader));
-    if (w < p.total) {
+  }
+  bool fresh = true;
+  while (w < p.total) {
+    if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
       const int i = w / p.n_games;
-      g = w % p.n_games;
+      const int g = w - i * p.n_games;
       kind = uniformize<L>(p.kind[w]);
       gr = genomes + (long)i * p.gstride;
       load_net<L, U, O, WT>(nr, gr, H, b, lig);
@@ -418,11 +510,8 @@ __global__ __launch_bounds__(256) void k_resident(EvalParams p) {
       }
       st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
       act_r = act_l = timeout = total = frames = 0;
+      fresh = false;
     }
-  };
-
-  start_game();
-  while (w < p.total) {
     const int s1b = st.s1, s2b = st.s2;
     const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
     st.step(act_r, act_l);
@@ -433,18 +522,13 @@ __global__ __launch_bounds__(256) void k_resident(EvalParams p) {
     int left = 0, right = 0;
     if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
       const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
-      if (kind == kOppNN) {
-        const int kl[6] = {320 - bx2, by2, 320 - lbx2, lby2, lc2, rc2};  // x flipped, main.py:146-147
-        left = decide<L, U, O, WT>(nl, gl, H, b, kl, lds, lig, slow);
-        c_fwd += 1;
-      } else if (kind == kOppScore) {
-        left = (st.s1 <= st.s2) ? hardcoded(by2, lc2) : 0;
-      } else {
-        left = hardcoded(by2, lc2);
-      }
       const int kr[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
-      right = decide<L, U, O, WT>(nr, gr, H, b, kr, lds, lig, slow);
-      c_fwd += 1;
+      const int kl[6] = {320 - bx2, by2, 320 - lbx2, lby2, lc2, rc2};  // x flipped, main.py:146-147
+      const bool left_nn = kind == kOppNN;
+      left = hardcoded(by2, lc2);
+      if (kind == kOppScore && st.s1 > st.s2) left = 0;
+      decide<L, U, O, WT>(nr, gr, kr, nl, gl, kl, left_nn, H, b, lds, lig, slow, right, left);
+      c_fwd += left_nn ? 2 : 1;
     }
     act_l = uniformize<L>(clamp_action(lc2, left));
     act_r = uniformize<L>(clamp_action(rc2, right));
@@ -462,7 +546,10 @@ __global__ __launch_bounds__(256) void k_resident(EvalParams p) {
       if (lig == 0) finish_game(p, w, st, frames, total);
       c_steps += frames;
       c_games += 1;
-      start_game();
+      int ww = 0;
+      if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
+      w = uniformize<L>(group_broadcast<L>(ww, leader));
+      fresh = true;
     }
   }
   if (p.counters && lig == 0 && c_games) {
@@ -538,27 +625,46 @@ __global__ __launch_bounds__(256) void k_forward_resident(FwdParams p) {
     const WT *gw = (const WT *)p.genomes + row * p.gstride;
     Net<U, O> net;
     load_net<L, U, O, WT>(net, gw, H, b, lig);
-    float x[6], z[O];
+    float x[6], acc[O], z[O];
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = (float)p.x[(long)t * 6 + i];
-    forward_f32<L, U, O>(net, x, z);
+    partial_f32<U, O>(net, x, acc);
+#pragma unroll
+    for (int o = 0; o < O; ++o) z[o] = group_sum<L>(acc[o]) + net.c[o];
     int idx = certify<O>(z, net.e);
     if (idx >= 0 && p.act) {
       // activations are reported within 2e-6: |S(z) - S(z_hat)| <= e * S'(max(|z_hat| - e, 0))
       bool tight = true;
 #pragma unroll
       for (int o = 0; o < O; ++o) {
-        const float t = fmaxf(fabsf(z[o]) - net.e[o], 0.f);
-        const float sp = __expf(-t) / ((1.f + __expf(-t)) * (1.f + __expf(-t)));
-        tight = tight && (net.e[o] * sp <= 2e-6f);
+        const float tt = fmaxf(fabsf(z[o]) - net.e, 0.f);
+        const float sp = __expf(-tt) / ((1.f + __expf(-tt)) * (1.f + __expf(-tt)));
+        tight = tight && (net.e * sp <= 2e-6f);
       }
       if (!tight) idx = -1;
     }
     if (idx < 0) {
-      double xd[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) xd[i] = p.x[(long)t * 6 + i];
-      idx = forward_f64_group<L, U, O, WT>(gw, H, b, xd, lds, lig);
+      // arbitrary f64 inputs here: run the f64 pass on them directly
+      const int cols = 6 + b;
+      for (int j = lig; j < H; j += L) {
+        const WT *r = gw + (long)j * cols;
+        double zz = 0.0;
+        for (int i = 0; i < 6; ++i) zz = __dadd_rn(zz, __dmul_rn((double)r[i], p.x[(long)t * 6 + i]));
+        if (b) zz = __dadd_rn(zz, (double)r[6]);
+        lds[j] = sigmoid_f64(zz);
+      }
+      wave_lds_sync();
+      if (lig < O) {
+        const WT *v = gw + (long)H * cols + (long)lig * (H + b);
+        double zz = 0.0;
+        for (int j = 0; j < H; ++j) zz = __dadd_rn(zz, __dmul_rn((double)v[j], lds[j]));
+        if (b) zz = __dadd_rn(zz, (double)v[H]);
+        lds[H + 1 + lig] = sigmoid_f64(zz);
+      }
+      wave_lds_sync();
+      idx = 0;
+      for (int o = 1; o < O; ++o)
+        if (lds[H + 1 + o] > lds[H + 1 + idx]) idx = o;
       if (p.act && lig < O) p.act[(long)t * O + lig] = lds[H + 1 + lig];
       wave_lds_sync();
       slow += (lig == 0);

@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_NAME = "libpong_ga.so"
-LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
 PG_ABI_VERSION = 1

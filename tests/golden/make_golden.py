@@ -365,6 +365,13 @@ def gen_helpers():
     fs = _find_stuff_np1(obs)
     h["find_stuff_obs"] = [list(map(float, v)) for v in fs]
     h["find_stuff_zero"] = [None if v is None else list(map(float, v)) for v in _find_stuff_np1(np.zeros_like(obs))]
+    # config.py surface: every upper-case name and its value
+    cfg = {}
+    for name in dir(ref_config):
+        if name.isupper():
+            v = getattr(ref_config, name)
+            cfg[name] = v.tolist() if isinstance(v, np.ndarray) else (list(v) if isinstance(v, tuple) else v)
+    h["config"] = cfg
     with open(os.path.join(HERE, "helpers.json"), "w") as fh:
         json.dump(h, fh, indent=0)
 

@@ -1,0 +1,113 @@
+"""The C-ABI boundary (include/pong_ga.h) without a GPU: the library loads,
+exports every declared entry point, the ctypes structures match the C layout
+byte for byte, and argument validation fails loudly before any HIP call."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "pong_ga.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from pong_amd import _lib
+    from pong_amd import build as B
+    B.build()
+    return _lib.lib()
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:char|int32_t|size_t)\s*\*?\s*(pg_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for must in ("pg_eval_population", "pg_forward", "pg_physics_step", "pg_physics_reset",
+                 "pg_last_error", "pg_version", "pg_ga_vary", "pg_ga_select_tournament"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from pong_amd import _lib
+    names = declared_functions()
+    for name in names:
+        assert hasattr(lib, name), f"{name} missing from {_lib.LIB_PATH}"
+    assert sorted(_lib.SIGNATURES) == names, "ctypes signatures out of sync with the header"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (pg_\w+)", out))
+    assert set(names) <= exported
+
+
+def test_version_and_gene_count(lib):
+    from pong_amd import _lib
+    assert lib.pg_abi_version() == _lib.PG_ABI_VERSION
+    assert b"gfx950" in lib.pg_version()
+    for shape, genes in (([6, 2, 2], 20), ([6, 64, 3], 643), ([6, 512, 512, 3], 267779)):
+        net = _lib.make_net(shape)
+        assert lib.pg_gene_count(ctypes.byref(net)) == genes
+
+
+def test_validation_errors_without_gpu(lib):
+    from pong_amd import _lib
+    assert lib.pg_eval_population(None, None) == _lib.PG_ERR_INVALID
+    assert b"NULL" in lib.pg_last_error()
+    a = _lib.PgEvalArgs()
+    a.net = _lib.make_net([5, 2, 2])
+    a.n_games = 6
+    assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_ERR_INVALID
+    assert b"6 inputs" in lib.pg_last_error()
+    a.net = _lib.make_net([6, 2, 2])
+    a.n_games = 0
+    assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_ERR_INVALID
+    a.n_games = 6
+    a.n_genomes = 0  # empty batch: nothing to do, no device touched
+    assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_OK
+    a.n_genomes = 4
+    a.genome_stride = 3  # < 20 genes
+    assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_ERR_INVALID
+    assert b"genome_stride" in lib.pg_last_error()
+    bad = _lib.make_net([6, 2, 2])
+    bad.n_nodes = 1
+    assert lib.pg_gene_count(ctypes.byref(bad)) == _lib.PG_ERR_INVALID
+    assert lib.pg_physics_step(None, -1, None, None) == _lib.PG_ERR_INVALID
+
+
+def test_struct_layout_matches_c(tmp_path):
+    """offsetof/sizeof of every ABI struct from gcc vs the ctypes mirror."""
+    from pong_amd import _lib
+    structs = {"pg_net": _lib.PgNet, "pg_eval_args": _lib.PgEvalArgs, "pg_forward_args": _lib.PgForwardArgs,
+               "pg_ga_args": _lib.PgGaArgs, "pg_select_args": _lib.PgSelectArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'  printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-o", str(exe), str(src)])
+    c = {}
+    for line in subprocess.check_output([str(exe)], text=True).splitlines():
+        s, f, v = line.split()
+        c[(s, f)] = int(v)
+    for cname, cls in structs.items():
+        assert c[(cname, "size")] == ctypes.sizeof(cls), cname
+        for fname, _ in cls._fields_:
+            assert c[(cname, fname)] == getattr(cls, fname).offset, f"{cname}.{fname}"
+
+
+def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
+    """The product path refuses to run without the HIP library."""
+    code = ("import sys; sys.path.insert(0, %r); from pong_amd import _lib; _lib.LIB_PATH = %r; "
+            "\ntry:\n    _lib.lib()\nexcept RuntimeError as e:\n    print('refused', e)" %
+            (os.path.join(REPO, "neuro-genetic-pong-self-play_amd"), str(tmp_path / "missing.so")))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
+    assert "refused" in out.stdout and "no CPU fallback" in out.stdout

@@ -1,0 +1,102 @@
+"""The drop-in surface on the MI355X (run with -m gpu): the reference's
+``toolbox.map(toolbox.evaluate, individuals)`` and ``NeuralNetwork.run``
+through ga.py / main.py / numpy_nn.py give the reference's own numbers."""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class _Fit:
+    def __init__(self, v):
+        self.values = (v,)
+        self.valid = True
+
+
+class _Member(list):
+    def __init__(self, genes, fit):
+        super().__init__(genes)
+        self.fitness = _Fit(fit)
+
+
+class _HoF:
+    def __init__(self, items):
+        self.items = items
+
+
+def test_toolbox_map_evaluate_matches_reference(gpu, golden):
+    """evaluate.json: fitness of the REAL evaluate() (incl. hall-of-fame games)."""
+    import ga
+    import main
+    import utils
+    saved = (utils.NETWORK_SHAPE, main.hall_of_fame)
+    try:
+        for case in golden("evaluate.json"):
+            utils.NETWORK_SHAPE = case["shape"]
+            main.hall_of_fame = _HoF([_Member(g, f) for g, f in zip(case["hof_genes"], case["hof_fitness"])])
+            random.seed(case["random_seed"])
+            inds = [list(g) for g in case["individuals"]]
+            got = [fit[0] for fit in ga.toolbox.map(ga.toolbox.evaluate, inds)]
+            assert got == case["fitness"]
+    finally:
+        utils.NETWORK_SHAPE, main.hall_of_fame = saved
+
+
+@pytest.mark.parametrize("key", ["6x2x2", "6x64x3", "6x8x8x3"])
+def test_neural_network_run_matches_reference(gpu, golden, key):
+    from numpy_nn import NeuralNetwork
+    g = golden("nn_forward.npz")
+    shape = [int(v) for v in g[f"{key}__shape"]]
+    genes, gidx, x = g[f"{key}__genes"], g[f"{key}__gidx"], g[f"{key}__x"]
+    for s in range(0, len(x), 37):  # a spread of samples: one device call each
+        net = NeuralNetwork(nodes=shape, weights=list(genes[gidx[s]]), bias=True)
+        action = net.run(list(x[s]))
+        idx = int(g[f"{key}__idx"][s])
+        assert action == ([1, 0] if idx == 0 else [0, 1] if idx == 1 else [0, 0])
+        np.testing.assert_allclose(net.list_of_transitional_arrays[-1][:-1], g[f"{key}__act"][s], atol=1e-5)
+
+
+def test_easimple_device_equals_sequential_oracle(gpu, oracle):
+    """Three generations of the reference's eaSimple (pop 64, [6,2,2]): the
+    batched device map and a sequential per-individual oracle evaluate draw the
+    same hall-of-fame opponents and produce identical populations and logs."""
+    import copy
+
+    import ga
+    import main
+    import utils
+    from pong_amd import schedule
+    from pong_amd.deap_compat import algorithms, tools
+
+    def oracle_evaluate(individual):
+        kind, opp, mult, members = schedule.reference_schedule(1, 6, main.hall_of_fame, utils.pick_hall_of_famer)
+        opps = np.array([list(m) for m in members]) if members else None
+        r = oracle.eval_population(np.array([list(individual)[:20]]), [6, 2, 2], kind, opp, mult, opponents=opps)
+        return (float(r["fitness"][0]),)
+
+    def run(evaluate_fn, map_fn):
+        tb = copy.copy(ga.toolbox)
+        tb.register("evaluate", evaluate_fn)
+        tb.register("map", map_fn)
+        random.seed(2024)
+        pop = tb.population(n=64)
+        hof = tools.HallOfFame(16)
+        main.hall_of_fame = hof
+        stats = tools.Statistics(lambda ind: ind.fitness.values)
+        stats.register("max", np.max)
+        stats.register("avg", np.mean)
+        pop, log = algorithms.eaSimple(pop, tb, cxpb=0.9, mutpb=0.9, ngen=3, stats=stats, halloffame=hof,
+                                       verbose=False)
+        return [list(i) for i in pop], [i.fitness.values for i in pop], list(log)
+
+    saved = main.hall_of_fame
+    try:
+        dev = run(main.evaluate, ga.toolbox.map)
+        seq = run(oracle_evaluate, map)
+    finally:
+        main.hall_of_fame = saved
+    assert dev[1] == seq[1]
+    assert dev[0] == seq[0]
+    assert dev[2] == seq[2]

@@ -16,4 +16,10 @@ ROOT=$(pwd)
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o kt --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof exit=$rc" >> "$OUT/summary.txt"; fatal $rc rocprof
+if [ -n "$PMC" ]; then
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$ROOT/$OUT/pmc_$ctr" -o pmc -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline "$@" > "$OUT/pmc_$ctr.json" 2> "$OUT/pmc_$ctr.err"
+    rc=$?; echo "pmc $ctr exit=$rc" >> "$OUT/summary.txt"; fatal $rc pmc
+  done
+fi
 exit 0
