@@ -196,7 +196,7 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / F32_VECTOR_PEAK_TFLOPS,
                          "traffic": None,
-                         "kernel": "k_resident (pg_eval_population)",
+                         "kernel": "k_service (pg_eval_population, split lanes + f64 service wave)",
                          "kernel_ms_per_launch": kernel_ms_mean,
                          "flops_per_forward": flops_per_forward,
                          "forwards_per_launch": fwd_per_launch,
@@ -217,7 +217,7 @@ def cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     O.build()
-    genomes = pop[: 1 << 14].double().cpu().numpy()
+    genomes = pop[lo:lo + (1 << 16)].double().cpu().numpy()
     opponents = hof.double().cpu().numpy()
     k, o, m = kind.cpu().numpy(), opp.cpu().numpy(), mult.cpu().numpy()
     steps, done, chunk = 0, 0, 256

@@ -70,9 +70,11 @@ typedef enum pg_precision {
 } pg_precision;
 
 typedef enum pg_kernel {
-  PG_KERNEL_AUTO = 0,
-  PG_KERNEL_GENERAL = 1,  /* one wave per game, f64, any NETWORK_SHAPE */
-  PG_KERNEL_RESIDENT = 2  /* weights resident in registers, [6, H<=256, 2..4] */
+  PG_KERNEL_AUTO = 0,      /* SPLIT when the shape and precision allow, else GENERAL */
+  PG_KERNEL_GENERAL = 1,   /* one wave per game, f64, any NETWORK_SHAPE */
+  PG_KERNEL_RESIDENT = 2,  /* [6, H<=256, 2..4]: one lane group holds both paddles' weights */
+  PG_KERNEL_SPLIT = 3      /* [6, H<=256, 2..4]: half a lane group per paddle's network, plus one
+                              f64 service wave per 1024-thread block for re-decisions */
 } pg_kernel;
 
 /* NETWORK_SHAPE (config.py:30-32) + BIAS (config.py:34) + genome storage type. */
@@ -109,7 +111,7 @@ typedef struct pg_eval_args {
   int32_t trace_games;           /* games (genome-major index g = i*n_games + game) traced */
   int32_t trace_cap;
   int32_t kernel;                /* pg_kernel */
-  int32_t group_lanes;           /* resident kernel lanes per game (4..64), 0 = auto */
+  int32_t group_lanes;           /* lanes per game of RESIDENT (4..64) / SPLIT (8..64), 0 = auto */
   void *workspace;               /* device scratch of pg_eval_workspace_bytes() bytes */
   size_t workspace_bytes;
 } pg_eval_args;

@@ -46,7 +46,7 @@ PG_HD double pg_exp_f64(double x) {
 /* 1 / (1 + pow(np.e, -z)) */
 PG_HD double pg_sigmoid_f64(double z) {
   double t = pg_exp_f64(-z);
-  t = fma(t, z * 5.318237706605891e-17, t);
+  if (t < INFINITY) t = fma(t, z * 5.318237706605891e-17, t);  /* inf * (1 + tiny) stays inf */
   return 1.0 / (1.0 + t);
 }
 

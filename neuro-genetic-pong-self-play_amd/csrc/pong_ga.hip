@@ -130,9 +130,9 @@ __device__ int forward_f64_wave(const WT *__restrict__ w, const int *nodes, int 
     nxt = t;
   }
   const int n_out = nodes[n_nodes - 1];
-  int best = 0;
-  for (int j = 1; j < n_out; ++j)
-    if (cur[j] > cur[best]) best = j;  // np.argmax: first maximum
+  int best = 0;  // np.argmax: the first NaN if any, else the first maximum
+  for (int j = 1; j < n_out && !__builtin_isnan(cur[best]); ++j)
+    if (__builtin_isnan(cur[j]) || cur[j] > cur[best]) best = j;
   return best;
 }
 
@@ -229,6 +229,10 @@ __global__ __launch_bounds__(64) void k_general(EvalParams p) {
 #ifndef PG_SLOW_INLINE
 #define PG_SLOW_INLINE __forceinline__
 #endif
+// hidden units whose weight loads are in flight together in load_net
+#ifndef PG_LOAD_BATCH
+#define PG_LOAD_BATCH 2
+#endif
 // minimum waves per SIMD requested from the register allocator (0 = no request)
 #ifndef PG_RES_WAVES
 #define PG_RES_WAVES 0
@@ -267,26 +271,37 @@ __device__ __forceinline__ void load_net(Net<U, O> &n, const WT *__restrict__ g,
     const int j = lig + L * u;
     const bool ok = j < H;
     const int jj = ok ? j : 0;  // padding units load a valid row and are zeroed
+    // Issue the unit's loads unconditionally, then mask arithmetically: a
+    // select on a load is turned into a branch around it by the backend,
+    // which serialises every load behind its own s_waitcnt.
+    WT raw[7 + O];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) raw[i] = g[(long)jj * cols + ((i < 6 || b) ? i : 0)];
+#pragma unroll
+    for (int o = 0; o < O; ++o) raw[7 + o] = g[off2 + (long)o * (H + b) + jj];
     float r = 0.f;
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
-      const int ii = (i < 6 || b) ? i : 0;
-      const float v = (float)g[(long)jj * cols + ii];
-      n.w1[u][i] = (ok && (i < 6 || b)) ? v : 0.f;
+      const float m = (ok && (i < 6 || b)) ? 1.f : 0.f;
+      n.w1[u][i] = (float)raw[i] * m;
       r += fabsf(n.w1[u][i]);
     }
 #pragma unroll
     for (int o = 0; o < O; ++o) {
-      const float v = (float)g[off2 + (long)o * (H + b) + jj];
-      n.w2[u][o] = ok ? v : 0.f;
+      n.w2[u][o] = (float)raw[7 + o] * (ok ? 1.f : 0.f);
       acc[o] += fabsf(n.w2[u][o]) * (3.f * r + 18.f);
     }
+    // bound the loads in flight (f64: 2 VGPRs each): this cold spot would
+    // otherwise set the register budget of the whole kernel
+    if ((u + 1) % PG_LOAD_BATCH == 0) __builtin_amdgcn_sched_barrier(0);
   }
+  WT rawc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) rawc[o] = g[off2 + (long)o * (H + b) + (b ? H : 0)];
   float e = 0.f;
 #pragma unroll
   for (int o = 0; o < O; ++o) {
-    const float v = (float)g[off2 + (long)o * (H + b) + (b ? H : 0)];
-    n.c[o] = b ? v : 0.f;
+    n.c[o] = (float)rawc[o] * (b ? 1.f : 0.f);
     e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + 13.f * fabsf(n.c[o])));
   }
   n.e = e;
@@ -320,65 +335,47 @@ __device__ __forceinline__ void partial_f32(const Net<U, O> &n, const float x[6]
 // margin below).  Returns -1 when the bound cannot prove the f64 decision;
 // the caller then recomputes the forward pass in f64.
 template <int O>
-__device__ __forceinline__ int certify_general(const float z[O], float e) {
-  int res = -2;  // -2: undecided yet
+__device__ __forceinline__ int certify(const float z[O], float e) {
+  // Branch-free: (a) the first output that may be saturated decides if it
+  // surely is (it ties at 1.0 with every later saturated one and beats every
+  // unsaturated one); (b) with none possibly saturated, the f32 winner must
+  // lead the runner-up by 2e plus the plateau width at its value.
+  constexpr float kTlo = 36.7367f, kThi = 36.7369f;
+  int sat_res = -2;  // -2: no output may be saturated
 #pragma unroll
-  for (int o = 0; o < O; ++o) {
-    if (res == -2 && !(z[o] + e < 36.7367f)) res = (z[o] - e > 36.7369f) ? o : -1;
+  for (int o = O - 1; o >= 0; --o) {
+    const bool maybe = !(z[o] + e < kTlo);  // NaN counts as "maybe"
+    const bool sure = z[o] - e > kThi;
+    sat_res = maybe ? (sure ? o : -1) : sat_res;
   }
-  if (res != -2) return res;
+  float top1 = z[0], top2 = -3.0e38f;
   int w = 0;
-  float zw = z[0];
 #pragma unroll
   for (int o = 1; o < O; ++o) {
-    const bool gt = z[o] > zw;
+    const bool gt = z[o] > top1;
+    top2 = gt ? top1 : fmaxf(top2, z[o]);
     w = gt ? o : w;
-    zw = gt ? z[o] : zw;
+    top1 = gt ? z[o] : top1;
   }
-  const float lo = zw - e;
-  const float tw = 8.8817842e-16f * (__expf(zw + e) + 1.0f);
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < O; ++k) ok = ok && (k == w || lo - (z[k] + e) > tw);
-  return ok ? w : -1;
-}
-
-template <int O>
-__device__ __forceinline__ int certify(const float z[O], float e) {
-  // common case: every output far below saturation (top + e < 20, where the
-  // plateau width is < 4.4e-7); the winner must lead the runner-up by 2e + that.
-  float top1, top2;
-  int w;
-  if constexpr (O == 2) {
-    w = z[1] > z[0] ? 1 : 0;
-    top1 = fmaxf(z[0], z[1]);
-    top2 = fminf(z[0], z[1]);
-  } else if constexpr (O == 3) {
-    top1 = fmaxf(fmaxf(z[0], z[1]), z[2]);
-    top2 = __builtin_amdgcn_fmed3f(z[0], z[1], z[2]);
-    w = (z[0] == top1) ? 0 : ((z[1] == top1) ? 1 : 2);
-  } else {
-    w = 0;
-    top1 = z[0];
-    top2 = -3.0e38f;
-#pragma unroll
-    for (int o = 1; o < O; ++o) {
-      const bool gt = z[o] > top1;
-      top2 = gt ? top1 : fmaxf(top2, z[o]);
-      w = gt ? o : w;
-      top1 = gt ? z[o] : top1;
-    }
-  }
+  const float tw = 8.8817842e-16f * (__expf(fminf(top1 + e, 40.f)) + 1.0f);
+  const int uns_res = (top1 - top2 > 2.f * e + tw) ? w : -1;
   float sum = 0.f;
 #pragma unroll
   for (int o = 0; o < O; ++o) sum += z[o];
-  if (sum == sum && top1 + e < 20.0f) return (top1 - top2 > 2.f * e + 4.4e-7f) ? w : -1;
-  return certify_general<O>(z, e);
+  if (sum != sum) return -1;  // a NaN output (non-finite weights): numpy's NaN rule in f64
+  return sat_res != -2 ? sat_res : uns_res;
 }
 
 // The f64 re-decision of one forward pass by the L lanes of a group, in
-// numpy_nn's order (sequential dot products), hidden activations in LDS.
-// Returns the argmax; leaves the output activations in lds[H+1 ..].
+// numpy_nn's order: each hidden unit a sequential dot product over
+// [x..., 1], each output a sequential sum of the products W2[o][j] * s_j.
+// The products are formed by all lanes in parallel (a product's rounding does
+// not depend on who computes it) and only the dependent additions run
+// serially, out of LDS -- no serial global loads.
+// LDS: lds[0, H) hidden activations, lds[H + o*(H+1) + j] products, then O
+// output activations; f64_lds_doubles(H, O) doubles in all.
+__host__ __device__ constexpr int f64_lds_doubles(int H, int O) { return H + O * (H + 1) + O + 1; }
+
 template <int L, int U, int O, typename WT>
 __device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H, int b, const int *k, double *lds,
                                               int lig) {
@@ -389,25 +386,36 @@ __device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H,
 #pragma unroll 1
   for (int j = lig; j < H; j += L) {
     const WT *row = g + (long)j * cols;
+    double w[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w[i] = (i < 6 || b) ? (double)row[i] : 0.0;
     double z = 0.0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], x[i]));
-    if (b) z = __dadd_rn(z, (double)row[6]);
+    for (int i = 0; i < 6; ++i) z = __dadd_rn(z, __dmul_rn(w[i], x[i]));
+    if (b) z = __dadd_rn(z, w[6]);
     lds[j] = pg_sigmoid_f64(z);
   }
   wave_lds_sync();
-  if (lig < O) {
-    const WT *v = g + (long)H * cols + (long)lig * (H + b);
-    double z = 0.0;
+  double *prod = lds + H;
+  const WT *v = g + (long)H * cols;
 #pragma unroll 1
-    for (int j = 0; j < H; ++j) z = __dadd_rn(z, __dmul_rn((double)v[j], lds[j]));
-    if (b) z = __dadd_rn(z, (double)v[H]);
-    lds[H + 1 + lig] = pg_sigmoid_f64(z);
+  for (int t = lig; t < O * (H + b); t += L) {
+    const int o = t / (H + b), j = t - o * (H + b);
+    const double wv = (double)v[(long)o * (H + b) + j];
+    prod[o * (H + 1) + j] = (j < H) ? __dmul_rn(wv, lds[j]) : wv;  // bias column times 1.0
   }
   wave_lds_sync();
-  int best = 0;
-  for (int o = 1; o < O; ++o)
-    if (lds[H + 1 + o] > lds[H + 1 + best]) best = o;
+  double *out = prod + O * (H + 1);
+  if (lig < O) {
+    const double *pr = prod + lig * (H + 1);
+    double z = 0.0;
+    for (int j = 0; j < H + b; ++j) z = __dadd_rn(z, pr[j]);
+    out[lig] = pg_sigmoid_f64(z);
+  }
+  wave_lds_sync();
+  int best = 0;  // np.argmax: the first NaN if any, else the first maximum
+  for (int o = 1; o < O && !__builtin_isnan(out[best]); ++o)
+    if (__builtin_isnan(out[o]) || out[o] > out[best]) best = o;
   wave_lds_sync();
   return best;
 }
@@ -420,16 +428,16 @@ __device__ __forceinline__ float feat32(int k) { return (float)k * 0.003125f; } 
 // Any undecided argmax is re-decided by ONE f64 code site (keeps the rare
 // path's registers and code out of the hot loop's way).
 template <int L, int U, int O, typename WT>
-__device__ __forceinline__ void decide(Net<U, O> &nr, const WT *gr, const int kr[6], Net<U, O> &nl,
-                                       const WT *gl, const int kl[6], bool left_nn, int H, int b, double *lds,
-                                       int lig, uint32_t &slow, int &right, int &left) {
-  float xr[6], ar[O], zr[O];
+__device__ __forceinline__ int2 decide(Net<U, O> &nr, const WT *gr, const int kr[6], Net<U, O> &nl,
+                                       const WT *gl, const int kl[6], bool left_nn, int left_scripted, int H,
+                                       int b, double *lds, int lig, uint32_t &slow) {
+  float xr[6], ar[O], zr[O], zl[O];
 #pragma unroll
   for (int i = 0; i < 6; ++i) xr[i] = feat32(kr[i]);
   partial_f32<U, O>(nr, xr, ar);
   int il = 0;
   if (left_nn) {
-    float xl[6], al[O], zl[O];
+    float xl[6], al[O];
 #pragma unroll
     for (int i = 0; i < 6; ++i) xl[i] = feat32(kl[i]);
     partial_f32<U, O>(nl, xl, al);
@@ -444,15 +452,17 @@ __device__ __forceinline__ void decide(Net<U, O> &nr, const WT *gr, const int kr
     for (int o = 0; o < O; ++o) zr[o] = group_sum<L>(ar[o]) + nr.c[o];
   }
   int ir = certify<O>(zr, nr.e);
+#ifdef PG_ABLATE_CERT  // timing-only build: plain f32 argmax, no certification
+  ir = zr[1] > zr[0] ? 1 : 0;
+  if (left_nn) il = zl[1] > zl[0] ? 1 : 0;
+#endif
   if (ir < 0 || il < 0) {  // rare and group-uniform
-#pragma unroll 1
-    for (int side = 0; side < 2; ++side) {
-      if ((side == 0 ? ir : il) >= 0) continue;
-      int k[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) k[i] = side ? kl[i] : kr[i];
-      const int idx = forward_f64_group<L, U, O, WT>(side ? gl : gr, H, b, k, lds, lig);
-      if (side) il = idx; else ir = idx;
+    if (il < 0) {
+      il = forward_f64_group<L, U, O, WT>(gl, H, b, kl, lds, lig);
+      slow += 1;
+    }
+    if (ir < 0) {
+      ir = forward_f64_group<L, U, O, WT>(gr, H, b, kr, lds, lig);
       slow += 1;
     }
     // Re-read the weights instead of keeping them live across the f64 pass:
@@ -460,8 +470,7 @@ __device__ __forceinline__ void decide(Net<U, O> &nr, const WT *gr, const int kr
     load_net<L, U, O, WT>(nr, gr, H, b, lig);
     if (left_nn) load_net<L, U, O, WT>(nl, gl, H, b, lig);
   }
-  right = index_to_code(ir);
-  if (left_nn) left = index_to_code(il);
+  return make_int2(index_to_code(ir), left_nn ? index_to_code(il) : left_scripted);
 }
 
 template <int L>
@@ -479,7 +488,7 @@ __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
   const int lig = threadIdx.x & (L - 1);
   const int grp = threadIdx.x / L;
   const int leader = lane64 & ~(L - 1);
-  double *lds = lds_all + grp * (H + 1 + O + 1);
+  double *lds = lds_all + grp * f64_lds_doubles(H, O);
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
 
@@ -525,9 +534,15 @@ __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
       const int kr[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
       const int kl[6] = {320 - bx2, by2, 320 - lbx2, lby2, lc2, rc2};  // x flipped, main.py:146-147
       const bool left_nn = kind == kOppNN;
-      left = hardcoded(by2, lc2);
-      if (kind == kOppScore && st.s1 > st.s2) left = 0;
-      decide<L, U, O, WT>(nr, gr, kr, nl, gl, kl, left_nn, H, b, lds, lig, slow, right, left);
+      int scripted = hardcoded(by2, lc2);
+      if (kind == kOppScore && st.s1 > st.s2) scripted = 0;
+#ifdef PG_ABLATE_NN  // timing-only build: scripted paddles on both sides, no network
+      const int2 d = make_int2(hardcoded(by2, rc2), scripted);
+#else
+      const int2 d = decide<L, U, O, WT>(nr, gr, kr, nl, gl, kl, left_nn, scripted, H, b, lds, lig, slow);
+#endif
+      right = d.x;
+      left = d.y;
       c_fwd += left_nn ? 2 : 1;
     }
     act_l = uniformize<L>(clamp_action(lc2, left));
@@ -558,6 +573,202 @@ __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
     atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
     atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
   }
+}
+
+// ================================================ split-lane helpers ==
+template <int L>
+__device__ __forceinline__ int other_half(int v) {
+  if constexpr (L == 8) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror: i <-> 7-i
+  } else if constexpr (L == 16) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror: i <-> 15-i
+  } else if constexpr (L == 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
+  }
+}
+
+// ============================================ split lanes + f64 service wave ==
+// k_split's layout, with the rare f64 re-decision moved to a dedicated wave:
+// a 1024-thread block runs 15 game waves and ONE service wave.  A half-group
+// whose certificate fails posts {genome, features} to an LDS mailbox and
+// sleeps until the service wave (64 lanes, numpy_nn order, f64) answers.  The
+// f64 code then lives in its own control-flow region, so it no longer sets
+// the game waves' register budget (which decides their occupancy).
+constexpr int kSvcThreads = 1024;
+constexpr int kSvcGameWaves = kSvcThreads / 64 - 1;
+
+struct SlowSlot {
+  const void *g;    // genome row of the network to re-decide
+  int k[6];         // its doubled-centroid features
+  int idx;          // answer: argmax index
+  volatile int flag;  // 0 free, 1 posted, 2 answered
+};
+
+template <int L, int U, int O, typename WT>
+__global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
+  constexpr int HL = L / 2;
+  constexpr int kSlots = kSvcGameWaves * (64 / L) * 2;
+  __shared__ SlowSlot slots[kSlots];
+  __shared__ int waves_done;
+  extern __shared__ double lds_svc[];  // f64_lds_doubles(H, O), service wave only
+  const int H = p.nodes[1];
+  const int b = p.bias;
+  const int wave = threadIdx.x >> 6;
+  const int lane64 = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < kSlots; i += kSvcThreads) slots[i].flag = 0;
+  if (threadIdx.x == 0) waves_done = 0;
+  __syncthreads();
+
+  if (wave == kSvcGameWaves) {
+    // ---------------- service wave: f64 re-decisions for the whole block ----
+    for (;;) {
+      bool served = false;
+      for (int base = 0; base < kSlots; base += 64) {
+        const int sidx = base + lane64;
+        const bool posted = sidx < kSlots && slots[sidx].flag == 1;
+        unsigned long long mask = __ballot(posted);
+        while (mask) {
+          const int sl = base + __builtin_ctzll(mask);
+          mask &= mask - 1;
+          __threadfence_block();
+          const WT *g = (const WT *)slots[sl].g;
+          int k[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) k[i] = slots[sl].k[i];
+          const int idx = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64);
+          if (lane64 == 0) {
+            slots[sl].idx = idx;
+            __threadfence_block();
+            slots[sl].flag = 2;
+          }
+          served = true;
+        }
+      }
+      if (!served) {
+        if (*(volatile int *)&waves_done == kSvcGameWaves) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    return;
+  }
+
+  // ---------------- game waves: k_split's loop --------------------------------
+  const int lig = threadIdx.x & (L - 1);
+  const int side = lig >= HL ? 1 : 0;  // 0: right paddle's network, 1: left paddle's
+  const int hl = lig & (HL - 1);
+  const int leader = lane64 & ~(L - 1);
+  SlowSlot *slot = &slots[(threadIdx.x / L) * 2 + side];
+  const WT *genomes = (const WT *)p.genomes;
+  const WT *opponents = (const WT *)p.opponents;
+
+  Net<U, O> net;
+  Pong st;
+  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
+  const WT *gm = genomes;
+  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0;
+
+  int w;
+  {
+    int ww = 0;
+    if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
+    w = group_broadcast<L>(ww, leader);
+  }
+  bool fresh = true;
+  while (w < p.total) {
+    if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
+      const int i = w / p.n_games;
+      const int g = w - i * p.n_games;
+      kind = p.kind[w];
+      const WT *gr = genomes + (long)i * p.gstride;
+      gm = (side && kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
+      load_net<HL, U, O, WT>(net, gm, H, b, hl);
+      st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
+      act_r = act_l = timeout = total = frames = 0;
+      fresh = false;
+    }
+    const int s1b = st.s1, s2b = st.s2;
+    const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
+    st.step(act_r, act_l);
+    frames += 1;
+    const int vis = st.vis;
+    const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
+    const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
+    int left = 0, right = 0;
+    if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
+      const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
+      // right side: [bx, by, lbx, lby, me=right, enemy=left]; left side x-flipped (main.py:146-147)
+      const int k[6] = {side ? 320 - bx2 : bx2, by2, side ? 320 - lbx2 : lbx2, lby2, side ? lc2 : rc2,
+                        side ? rc2 : lc2};
+      float x[6], acc[O], z[O];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) x[i] = feat32(k[i]);
+      partial_f32<U, O>(net, x, acc);
+#pragma unroll
+      for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
+      int idx = certify<O>(z, net.e);
+      const bool left_nn = kind == kOppNN;
+      if (side && !left_nn) idx = 0;  // the left half is idle against a scripted opponent
+#ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
+      if (idx < 0) idx = z[1] > z[0] ? 1 : 0;
+#endif
+      if (idx < 0) {  // rare, half-uniform: ask the service wave for the f64 decision
+        if (hl == 0) {
+          slot->g = gm;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) slot->k[i] = k[i];
+          __threadfence_block();
+          slot->flag = 1;
+        }
+        while (slot->flag != 2) __builtin_amdgcn_s_sleep(1);
+        __threadfence_block();
+        idx = slot->idx;
+        if (hl == 0) slot->flag = 0;
+        slow += 1;
+      }
+      const int mine = index_to_code(idx);
+      const int other = other_half<L>(mine);
+      right = side ? other : mine;
+      int scripted = hardcoded(by2, lc2);
+      if (kind == kOppScore && st.s1 > st.s2) scripted = 0;
+      left = left_nn ? (side ? mine : other) : scripted;
+      c_fwd += left_nn ? 2 : 1;
+    }
+    act_l = clamp_action(lc2, left);
+    act_r = clamp_action(rc2, right);
+    if (p.trace && w < p.trace_games && frames <= p.trace_cap && lig == 0)
+      p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+    if (frames > 1) {
+      if (st.s1 == s1b && st.s2 == s2b) {
+        timeout += 1;
+      } else {
+        total += timeout;
+        timeout = 0;
+      }
+    }
+    if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
+      if (lig == 0) finish_game(p, w, st, frames, total);
+      c_steps += frames;
+      c_games += 1;
+      int ww = 0;
+      if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
+      w = group_broadcast<L>(ww, leader);
+      fresh = true;
+    }
+  }
+  if (p.counters && c_games) {
+    if (lig == 0) {
+      atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)c_steps);
+      atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
+      atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
+    }
+    if (hl == 0 && slow) atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
+  }
+  // this wave will post no more requests
+  if (lane64 == 0) atomicAdd(&waves_done, 1);
 }
 
 // ------------------------------------------------------------- fitness ----
@@ -662,9 +873,9 @@ __global__ __launch_bounds__(256) void k_forward_resident(FwdParams p) {
         lds[H + 1 + lig] = sigmoid_f64(zz);
       }
       wave_lds_sync();
-      idx = 0;
-      for (int o = 1; o < O; ++o)
-        if (lds[H + 1 + o] > lds[H + 1 + idx]) idx = o;
+      idx = 0;  // np.argmax: the first NaN if any, else the first maximum
+      for (int o = 1; o < O && !__builtin_isnan(lds[H + 1 + idx]); ++o)
+        if (__builtin_isnan(lds[H + 1 + o]) || lds[H + 1 + o] > lds[H + 1 + idx]) idx = o;
       if (p.act && lig < O) p.act[(long)t * O + lig] = lds[H + 1 + lig];
       wave_lds_sync();
       slow += (lig == 0);
@@ -866,7 +1077,7 @@ static ResidentChoice choose_resident(int H, int requested_L) {
 template <int L, int U, int O, typename WT>
 static int32_t launch_resident(const EvalParams &p, hipStream_t s) {
   constexpr int GPB = 256 / L;
-  const size_t lds = (size_t)GPB * (p.nodes[1] + 1 + O + 1) * sizeof(double);
+  const size_t lds = (size_t)GPB * f64_lds_doubles(p.nodes[1], O) * sizeof(double);
   const int want = (p.total + GPB - 1) / GPB;
   const int cap = num_cus() * 8;
   const int grid = want < cap ? want : cap;
@@ -874,6 +1085,43 @@ static int32_t launch_resident(const EvalParams &p, hipStream_t s) {
   hipLaunchKernelGGL((k_resident<L, U, O, WT>), dim3(grid), dim3(256), lds, s, p);
   PG_HIP(hipGetLastError());
   return PG_OK;
+}
+
+// split layout for hidden width H: L lanes per game (L/2 per network) with
+// the fewest units per lane that keep the group within L/2 lanes of work
+static int choose_split_lanes(int H) {
+  if (H <= 4) return 8;
+  if (H <= 16) return 16;
+  if (H <= 64) return 32;
+  return 64;
+}
+
+template <int L, int U, int O, typename WT>
+static int32_t launch_service(const EvalParams &p, hipStream_t s) {
+  constexpr int GPB = kSvcGameWaves * (64 / L);  // game groups per block
+  const size_t lds = (size_t)f64_lds_doubles(p.nodes[1], O) * sizeof(double);
+  const int want = (p.total + GPB - 1) / GPB;
+  const int cap = num_cus() * 2;
+  const int grid = want < cap ? want : cap;
+  if (grid <= 0) return PG_OK;
+  hipLaunchKernelGGL((k_service<L, U, O, WT>), dim3(grid), dim3(kSvcThreads), lds, s, p);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+template <typename WT>
+static int32_t launch_service_any(const EvalParams &p, int L, int O, hipStream_t s) {
+  const int H = p.nodes[1];
+#define PG_SVC(LL, UU)                                                   \
+  if (L == LL && (LL / 2) * UU >= H) {                                   \
+    if (O == 2) return launch_service<LL, UU, 2, WT>(p, s);              \
+    if (O == 3) return launch_service<LL, UU, 3, WT>(p, s);              \
+    if (O == 4) return launch_service<LL, UU, 4, WT>(p, s);              \
+  }
+  PG_SVC(8, 1) PG_SVC(8, 2) PG_SVC(16, 1) PG_SVC(16, 2) PG_SVC(16, 4) PG_SVC(16, 8)
+  PG_SVC(32, 1) PG_SVC(32, 2) PG_SVC(32, 4) PG_SVC(32, 8) PG_SVC(64, 1) PG_SVC(64, 2) PG_SVC(64, 4) PG_SVC(64, 8)
+#undef PG_SVC
+  return fail(PG_ERR_UNSUPPORTED, "no service kernel for L=%d H=%d O=%d", L, H, O);
 }
 
 template <int L, int U, typename WT>
@@ -1015,8 +1263,16 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   PG_HIP(hipMemsetAsync(a->workspace, 0, 256, s));
   int kernel = a->kernel;
   const bool res_ok = resident_shape_ok(a->net);
-  if (kernel == PG_KERNEL_AUTO) kernel = (res_ok && a->precision == PG_PREC_CERTIFIED) ? PG_KERNEL_RESIDENT : PG_KERNEL_GENERAL;
-  if (kernel == PG_KERNEL_RESIDENT) {
+  if (kernel == PG_KERNEL_AUTO) kernel = (res_ok && a->precision == PG_PREC_CERTIFIED) ? PG_KERNEL_SPLIT : PG_KERNEL_GENERAL;
+  if (kernel == PG_KERNEL_SPLIT) {
+    if (!res_ok) return fail(PG_ERR_UNSUPPORTED, "split kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
+    if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "split kernel is the certified-precision path");
+    const int H = a->net.nodes[1];
+    const int L = a->group_lanes > 0 ? a->group_lanes : choose_split_lanes(H);
+    rc = a->net.dtype == PG_F64 ? launch_service_any<double>(p, L, a->net.nodes[2], s)
+                                : launch_service_any<float>(p, L, a->net.nodes[2], s);
+    if (rc != PG_OK) return rc;
+  } else if (kernel == PG_KERNEL_RESIDENT) {
     if (!res_ok) return fail(PG_ERR_UNSUPPORTED, "resident kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
     if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "resident kernel is the certified-precision path");
     const ResidentChoice c = choose_resident(a->net.nodes[1], a->group_lanes);

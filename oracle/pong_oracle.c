@@ -179,9 +179,9 @@ int or_nn_run(const double *genes, const or_net *net, const double *x, double *o
     nxt = t;
   }
   const int n_out = net->nodes[net->n_nodes - 1];
-  int best = 0;
-  for (int j = 1; j < n_out; ++j)
-    if (cur[j] > cur[best]) best = j; /* np.argmax: first maximum wins */
+  int best = 0; /* np.argmax: the first NaN if any, else the first maximum */
+  for (int j = 1; j < n_out && !isnan(cur[best]); ++j)
+    if (isnan(cur[j]) || cur[j] > cur[best]) best = j;
   if (out_act)
     for (int j = 0; j < n_out; ++j) out_act[j] = cur[j];
   return best;

@@ -160,22 +160,28 @@ def test_eval_matches_oracle(gpu, oracle, shape, dist):
     res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
     _assert_same(res, ref)
     assert int(res.counters[0]) == int(ref["frames"].sum())
-    if len(shape) == 3:  # the f64 general kernel must agree too
-        res2, _ = ev.evaluate(_dev_genomes(genomes, gpu), torch.tensor(kinds, device=gpu),
-                              torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
-                              opponents=_dev_genomes(opponents, gpu), kernel="general", precision="f64")
-        _assert_same(res2, ref)
+    if len(shape) == 3:  # the other kernels must agree too
+        for kernel, precision in (("general", "f64"), ("resident", "certified")):
+            res2, _ = ev.evaluate(_dev_genomes(genomes, gpu), torch.tensor(kinds, device=gpu),
+                                  torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
+                                  opponents=_dev_genomes(opponents, gpu), kernel=kernel, precision=precision)
+            _assert_same(res2, ref)
 
 
-@pytest.mark.parametrize("lanes", [4, 8, 16, 32, 64])
-def test_eval_group_lanes_variants(gpu, oracle, lanes):
+@pytest.mark.parametrize("kernel,lanes,hidden", [
+    ("resident", 4, 4), ("resident", 8, 8), ("resident", 16, 16), ("resident", 32, 32), ("resident", 64, 64),
+    ("resident", 16, 64), ("resident", 32, 64), ("resident", 64, 200),
+    ("split", 8, 4), ("split", 8, 8), ("split", 16, 16), ("split", 16, 64), ("split", 32, 64),
+    ("split", 64, 64), ("split", 64, 256), ("split", 32, 50)])
+def test_eval_kernel_layouts(gpu, oracle, kernel, lanes, hidden):
+    """Every lane layout of both register-resident kernels vs the oracle."""
     from pong_amd.device import Evaluator
-    shape = [6, 4, 3] if lanes == 4 else [6, min(lanes, 64), 3]
-    rng = np.random.default_rng(lanes)
+    shape = [6, hidden, 3]
+    rng = np.random.default_rng(lanes * 1000 + hidden)
     G = _gene_count(shape)
     genomes, opponents = rng.standard_normal((64, G)), rng.standard_normal((7, G))
     kinds, opp, mult = _schedule(rng, 64, 6, 7)
-    ev = Evaluator(shape, device=gpu, group_lanes=lanes, kernel="resident")
+    ev = Evaluator(shape, device=gpu, group_lanes=lanes, kernel=kernel)
     res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
     _assert_same(res, ref)
 

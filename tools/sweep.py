@@ -68,7 +68,7 @@ def main():
             env = dict(os.environ)
             if lib:
                 env["PONG_GA_LIB"] = os.path.abspath(lib)
-            cmd = [sys.executable, __file__, "--one", "--lane", str(lane), "--reps", str(args.reps),
+            cmd = [sys.executable, __file__, "--one", f"--lane={lane}", "--reps", str(args.reps),
                    "--pop", str(args.pop), "--shape", args.shape, "--sigma", str(args.sigma), "--dtype", args.dtype]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
