@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 1
+#define PG_ABI_VERSION 2
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -106,7 +106,9 @@ typedef struct pg_eval_args {
   int32_t *frames;               /* [n_genomes, n_games] env.step calls */
   double *total_frames;          /* [n_genomes, n_games] main.py:73 accumulator */
   int32_t *status;               /* [n_genomes] 1 = ZeroDivisionError in calculate_reward */
-  uint64_t *counters;            /* optional [4]: env steps, NN forwards, f64 re-decisions, games */
+  uint64_t *counters;            /* optional [6]: env steps, NN forwards, full f64 forwards, games,
+                                    f32 certificate failures, failures decided by the plateau rule
+                                    (the split kernel; the others leave [4], [5] untouched) */
   uint8_t *trace;                /* optional [trace_games, trace_cap] per-frame action codes */
   int32_t trace_games;           /* games (genome-major index g = i*n_games + game) traced */
   int32_t trace_cap;
@@ -130,7 +132,7 @@ typedef struct pg_forward_args {
   int32_t precision;             /* pg_precision */
   int32_t *index;                /* [n] np.argmax of the output activations */
   double *act;                   /* optional [n, nodes[last]] output activations */
-  uint64_t *counters;            /* optional [4], as pg_eval_args */
+  uint64_t *counters;            /* optional [4]: [2] += passes re-decided in f64 (others unused) */
 } pg_forward_args;
 
 /* Struct-of-arrays game state: int32 [PG_STATE_FIELDS, n], field f of game i

@@ -62,59 +62,59 @@ struct Pong {
 
   __device__ bool done() const { return s1 >= kDoneScore || s2 >= kDoneScore; }
 
-  __device__ static int move(int y, int code, int speed) {
-    // code: 0 = [0,0], 1 = [1,0] up, 2 = [0,1] down, 3 = [1,1] (no motion)
-    y += (code == 1) ? -speed : ((code == 2) ? speed : 0);
-    return clampi(y, kPaddleYMin, kPaddleYMax);
+  __device__ static int dy_of(int code) {  // code: 0 = [0,0], 1 = [1,0] up, 2 = [0,1] down, 3 = [1,1]
+    return (code == 2) - (code == 1);
+  }
+  __device__ static int move(int y, int dy, int speed) {
+    return min(max(y + dy * speed, kPaddleYMin), kPaddleYMax);  // one v_med3_i32
   }
 
   // env.step(action) (main.py:77): right [up,down] = action[4:6], left = action[6:8].
+  // Branch-free except the serve (once per point): every game of a lane group
+  // runs the same instruction stream, so divergent branches would cost both sides.
   __device__ void step(int right_code, int left_code) {
-    rpy = move(rpy, right_code, kPaddleSpeed);
-    if (one_player) {
-      int code = 0;
-      if (vis) {
-        const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
-        code = (bc2 < pc2 - 4) ? 1 : ((bc2 > pc2 + 4) ? 2 : 0);
-      }
-      lpy = move(lpy, code, kCpuSpeed);
-    } else {
-      lpy = move(lpy, left_code, kPaddleSpeed);
-    }
-    if (!vis) {
-      if (timer > 0) timer -= 1;
-      if (timer == 0 && !done()) serve();
-      return;
-    }
-    int nx = bx + vx, ny = by + vy, nvx = vx, nvy = vy;
+    rpy = move(rpy, dy_of(right_code), kPaddleSpeed);
+    // left paddle: the action, or the built-in CPU of the 1-player env (main.py:40)
+    const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
+    const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
+    lpy = move(lpy, one_player ? cpu_dy : dy_of(left_code), one_player ? kCpuSpeed : kPaddleSpeed);
+
+    // ball in play: move, walls, paddle faces
     constexpr int ymax = kFieldH - kBallH;
-    if (ny < 0) {
-      ny = -ny;
-      nvy = -nvy;
-    } else if (ny > ymax) {
-      ny = 2 * ymax - ny;
-      nvy = -nvy;
-    }
     constexpr int lface = kLeftPaddleX + kPaddleW, rface = kRightPaddleX;
+    int nx = bx + vx, ny = by + vy;
+    const bool wall_top = ny < 0, wall_bot = ny > ymax;
+    ny = wall_top ? -ny : (wall_bot ? 2 * ymax - ny : ny);
+    const int wvy = (wall_top || wall_bot) ? -vy : vy;
     const bool to_left = (vx < 0) && (nx <= lface - 1);
     const bool to_right = (vx > 0) && (nx + kBallW - 1 >= rface);
-    if (to_left || to_right) {
-      const int py = to_left ? lpy : rpy;
-      if (ny <= py + kPaddleH - 1 && ny + kBallH - 1 >= py) {  // bounce
-        hits += 1;
-        int mag = kBallVx0 + hits / 4;
-        mag = mag > kBallVxMax ? kBallVxMax : mag;
-        nx = to_left ? lface : rface - kBallW;
-        nvx = to_left ? mag : -mag;
-        nvy = (2 * (ny - py) - 12) / 6;  // truncation toward zero
-      } else {  // miss: the other side scores, the ball disappears until the next serve
-        if (to_left) { s2 += 1; dir = -1; } else { s1 += 1; dir = 1; }
-        vis = 0;
-        timer = kServeDelay;
-        return;
-      }
+    const int py = to_left ? lpy : rpy;
+    const bool overlap = (ny <= py + kPaddleH - 1) && (ny + kBallH - 1 >= py);
+    const bool hit = vis && (to_left || to_right) && overlap;
+    const bool miss = vis && (to_left || to_right) && !overlap;
+    const int nhits = hits + (hit ? 1 : 0);
+    const int mag = min(kBallVx0 + (nhits >> 2), kBallVxMax);
+    // (2 (ny - py) - 12) / 6 truncated toward zero; |d| <= 18 is even, so |d| / 6 == (|d| * 43) >> 8
+    const int d = 2 * (ny - py) - 12;
+    const int q = (abs(d) * 43) >> 8;
+    const int hvy = d < 0 ? -q : q;
+    if (vis && !miss) {  // a miss leaves the ball where it was (hidden until the serve)
+      bx = hit ? (to_left ? lface : rface - kBallW) : nx;
+      by = ny;
+      vx = hit ? (to_left ? mag : -mag) : vx;
+      vy = hit ? hvy : wvy;
     }
-    bx = nx; by = ny; vx = nvx; vy = nvy;
+    hits = nhits;
+    // a miss scores for the other side and hides the ball until the next serve
+    s2 += (miss && to_left) ? 1 : 0;
+    s1 += (miss && to_right) ? 1 : 0;
+    dir = miss ? (to_left ? -1 : 1) : dir;
+    // ball hidden: the serve timer runs down (the frame of a miss only starts it)
+    const int t = vis ? timer : (timer > 0 ? timer - 1 : 0);
+    timer = miss ? kServeDelay : t;
+    const bool do_serve = !vis && t == 0 && !done();
+    vis = (vis && !miss) ? 1 : 0;
+    if (do_serve) serve();
   }
 
   __device__ void serve() {

@@ -328,6 +328,113 @@ __device__ __forceinline__ void partial_f32(const Net<U, O> &n, const float x[6]
   }
 }
 
+// ---- packed layout of the split kernel -------------------------------------
+// Units in pairs (u = 2p, 2p+1) as float2, so the hidden layer runs on
+// v_pk_fma_f32: one instruction advances two independent dot products, which
+// halves the issue count and the length of the dependent chain per frame.
+// W1 is stored pre-scaled by -log2(e) / 320 (feature columns; the features
+// then enter as the exact integers k) and -log2(e) (bias column), so the
+// pre-activation feeds v_exp_f32 directly: a' = -a log2 e.  Each stored
+// weight carries one more rounding (<= 2u relative in all), and the fma chain
+// over exact inputs stays within the 11u R_j hidden-error term of load_net.
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+template <int U, int O>
+struct NetP {
+  static constexpr int P = (U + 1) / 2;  // unit pairs
+  float2v w1[P][7];  // pre-scaled input weights (6 features + bias) of units 2p, 2p+1
+  float2v w2[P][O];  // output weights of the pair
+  float c[O];        // output biases
+  float e;           // certified bound, as Net::e
+};
+
+// Number of f32 roundings in one output sum of the packed forward: a chain of
+// P pk_fma per component, the .x + .y fold, the group tree, + c, and the
+// f32 rounding of W2 -- bounded by U + log2(HL) + 3 for every layout.
+template <int HL, int U>
+__host__ __device__ constexpr int out_roundings() {
+  return U + (HL >= 32 ? 5 : HL >= 16 ? 4 : HL >= 8 ? 3 : HL >= 4 ? 2 : HL >= 2 ? 1 : 0) + 3;
+}
+
+template <int L, int U, int O, typename WT>
+__device__ __forceinline__ void load_net_pk(NetP<U, O> &n, const WT *__restrict__ g, int H, int b, int lig) {
+  constexpr int P = NetP<U, O>::P;
+  constexpr float kScaleX = -1.4426950408889634f / 320.f;
+  constexpr float kScaleB = -1.4426950408889634f;
+  const int cols = 6 + b;
+  const long off2 = (long)H * cols;
+  float acc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = 2 * p + h;
+      const int j = lig + L * u;
+      const bool ok = u < U && j < H;
+      const int jj = ok ? j : 0;  // padding units load a valid row and are zeroed
+      WT raw[7 + O];  // unconditional loads, masked arithmetically (see load_net)
+#pragma unroll
+      for (int i = 0; i < 7; ++i) raw[i] = g[(long)jj * cols + ((i < 6 || b) ? i : 0)];
+#pragma unroll
+      for (int o = 0; o < O; ++o) raw[7 + o] = g[off2 + (long)o * (H + b) + jj];
+      float r = 0.f;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const float w = (float)raw[i] * ((ok && (i < 6 || b)) ? 1.f : 0.f);
+        r += fabsf(w);
+        n.w1[p][i][h] = w * (i < 6 ? kScaleX : kScaleB);
+      }
+#pragma unroll
+      for (int o = 0; o < O; ++o) {
+        const float w = (float)raw[7 + o] * (ok ? 1.f : 0.f);
+        n.w2[p][o][h] = w;
+        acc[o] += fabsf(w) * (3.f * r + 5.f + (float)out_roundings<L, U>());
+      }
+    }
+    if ((p + 1) % PG_LOAD_BATCH == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+  WT rawc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) rawc[o] = g[off2 + (long)o * (H + b) + (b ? H : 0)];
+  float e = 0.f;
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    n.c[o] = (float)rawc[o] * (b ? 1.f : 0.f);
+    e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + (float)out_roundings<L, U>() * fabsf(n.c[o])));
+  }
+  n.e = e;
+}
+
+// Hidden layer and the lane-partial output sums of one packed network; k are
+// the six doubled-centroid features (x_i = k_i / 320 is folded into W1).
+template <int U, int O>
+__device__ __forceinline__ void partial_pk(const NetP<U, O> &n, const int k[6], float acc[O]) {
+  constexpr int P = NetP<U, O>::P;
+  float2v kx[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const float f = (float)k[i];
+    kx[i] = float2v{f, f};
+  }
+  float2v a2[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) a2[o] = float2v{0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    float2v a = n.w1[p][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a = __builtin_elementwise_fma(n.w1[p][i], kx[i], a);
+    float2v q = float2v{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
+    const float2v sg = float2v{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+#pragma unroll
+    for (int o = 0; o < O; ++o) a2[o] = __builtin_elementwise_fma(n.w2[p][o], sg, a2[o]);
+  }
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = a2[o].x + a2[o].y;
+}
+
 // Certified argmax of S(z) = 1/(1 + pow(e, -z)) in f64 (numpy_nn.py:22-23,131)
 // given |z_true - z[o]| <= e.  S is exactly 1.0 iff z >= 53 ln 2 =
 // 36.73680056967710 (then every saturated output ties and the first wins);
@@ -593,23 +700,102 @@ __device__ __forceinline__ int other_half(int v) {
 
 // ============================================ split lanes + f64 service wave ==
 // k_split's layout, with the rare f64 re-decision moved to a dedicated wave:
-// a 1024-thread block runs 15 game waves and ONE service wave.  A half-group
+// a block (svc_threads) runs its game waves and ONE service wave.  A half-group
 // whose certificate fails posts {genome, features} to an LDS mailbox and
 // sleeps until the service wave (64 lanes, numpy_nn order, f64) answers.  The
 // f64 code then lives in its own control-flow region, so it no longer sets
 // the game waves' register budget (which decides their occupancy).
-constexpr int kSvcThreads = 1024;
-constexpr int kSvcGameWaves = kSvcThreads / 64 - 1;
+// Block size by register budget: a game lane holds 10U + 4 weight floats, so
+// U <= 4 fits 128 VGPRs (4 waves/SIMD: 16-wave blocks), U = 8 fits 168
+// (3 waves/SIMD: 12-wave blocks), U = 16 fits 256 (2 waves/SIMD: 8-wave blocks).
+// One block per CU either way; PG_SVC_NT forces one size (experiments).
+template <int U>
+__host__ __device__ constexpr int svc_threads() {
+#ifdef PG_SVC_NT
+  return PG_SVC_NT;
+#else
+  return U <= 4 ? 1024 : (U <= 8 ? 768 : 512);
+#endif
+}
+
+// A game whose rally settles into a periodic orbit meets the same near-tie
+// states every period; without a memo each costs a round trip to the service
+// wave (~3 us), and such games ran 3-4x slower per frame and set the launch's
+// tail (tools/timeline.py).  The memo holds the network's last kMemo f64
+// decisions keyed by the packed features -- the decision is a pure function
+// of (network, features), so a hit is exact.  Cleared at every game start.
+constexpr int kMemo = 8;
 
 struct SlowSlot {
   const void *g;    // genome row of the network to re-decide
   int k[6];         // its doubled-centroid features
+  float z[4];       // the f32 output pre-activations and their bound e
+  float e;
   int idx;          // answer: argmax index
   volatile int flag;  // 0 free, 1 posted, 2 answered
+  volatile int n_memo;  // decisions memoised for the current game's network
+  volatile uint64_t memo_key[kMemo];
+  volatile int memo_idx[kMemo];
 };
 
+// Plateau certificate, tried by the service wave before a full f64 forward.
+// For z >= 22.2, numpy's S(z) = 1/(1 + pow(e, -z)) is exactly
+// 1 - m(z) 2^-52 with m(z) = rint(2^52 pow(e, -z)) (1 + p rounds to
+// 1 + m 2^-52; its reciprocal rounds to 1 - m 2^-52 while m < 2^20), so two
+// outputs tie iff their m are equal and the larger S is the smaller m.  m is
+// monotone in z, so with |z_true - z| <= e the f32 outputs bound each m
+// between m(z + e) and m(z - e).  This decides the near-saturation rallies
+// whose plateaus are too wide for certify()'s gap test.  Lanes 0..2O-1 each
+// evaluate one endpoint; returns -1 when undecided (the full f64 path runs).
+template <int O>
+__device__ int plateau_decide(const float *z, float e, int lane) {
+  constexpr int kBig = 0x7fffffff;  // "below the plateau regime": worse than any m
+  int m = kBig;
+  bool amb = false;
+  if (lane < 2 * O) {
+    const int o = lane >> 1;
+    const double zz = (double)z[o] + ((lane & 1) ? (double)e : -(double)e);
+    if (zz != zz) {
+      amb = true;  // NaN: numpy's NaN rule, in the f64 path
+    } else if (zz >= 22.2) {
+      double t = pg_exp_f64(-zz);
+      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z), as pg_sigmoid_f64
+      const double v = t * 4503599627370496.0;    // 2^52 p
+      const double fr = v - floor(v);
+      amb = fabs(fr - 0.5) < 1e-6;  // too close to a rounding boundary to call
+      m = (int)rint(v);
+    }
+  }
+  if (__ballot(amb)) return -1;
+  int mlo[O], mhi[O];  // m(z + e) <= m_true <= m(z - e)
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    mhi[o] = __builtin_amdgcn_readlane(m, 2 * o);
+    mlo[o] = __builtin_amdgcn_readlane(m, 2 * o + 1);
+  }
+#pragma unroll
+  for (int w = 0; w < O; ++w) {
+    bool ok = mhi[w] != kBig;
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+      if (o != w) ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
+    if (ok) return w;
+  }
+  return -1;
+}
+
+// the six doubled-centroid features, each in [0, 512), as one 54-bit key
+__device__ __forceinline__ uint64_t memo_key(const int k[6]) {
+  uint64_t key = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) key = (key << 9) | (uint64_t)(k[i] & 511);
+  return key;
+}
+
 template <int L, int U, int O, typename WT>
-__global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
+__global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
+  constexpr int kSvcThreads = svc_threads<U>();
+  constexpr int kSvcGameWaves = kSvcThreads / 64 - 1;
   constexpr int HL = L / 2;
   constexpr int kSlots = kSvcGameWaves * (64 / L) * 2;
   __shared__ SlowSlot slots[kSlots];
@@ -639,7 +825,13 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
           int k[6];
 #pragma unroll
           for (int i = 0; i < 6; ++i) k[i] = slots[sl].k[i];
-          const int idx = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64);
+          float z[O];
+#pragma unroll
+          for (int o = 0; o < O; ++o) z[o] = slots[sl].z[o];
+          int idx = plateau_decide<O>(z, slots[sl].e, lane64);
+          // bit 8 / bit 9 of the answer: decided by a full f64 forward / by the plateau rule
+          idx = idx < 0 ? (256 | forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64))
+                        : (512 | idx);
           if (lane64 == 0) {
             slots[sl].idx = idx;
             __threadfence_block();
@@ -661,15 +853,17 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
   const int side = lig >= HL ? 1 : 0;  // 0: right paddle's network, 1: left paddle's
   const int hl = lig & (HL - 1);
   const int leader = lane64 & ~(L - 1);
-  SlowSlot *slot = &slots[(threadIdx.x / L) * 2 + side];
+  // index (not a pointer) into the __shared__ array keeps every mailbox access
+  // a ds_* instruction; a SlowSlot * decays to a flat pointer
+  const int sx = (threadIdx.x / L) * 2 + side;
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
 
-  Net<U, O> net;
+  NetP<U, O> net;
   Pong st;
   int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
   const WT *gm = genomes;
-  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0;
+  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0;
 
   int w;
   {
@@ -678,6 +872,9 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
     w = group_broadcast<L>(ww, leader);
   }
   bool fresh = true;
+#ifdef PG_TIMELINE
+  uint64_t t_start = 0;
+#endif
   while (w < p.total) {
     if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
       const int i = w / p.n_games;
@@ -685,10 +882,14 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
       kind = p.kind[w];
       const WT *gr = genomes + (long)i * p.gstride;
       gm = (side && kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
-      load_net<HL, U, O, WT>(net, gm, H, b, hl);
+      load_net_pk<HL, U, O, WT>(net, gm, H, b, hl);
       st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
       act_r = act_l = timeout = total = frames = 0;
       fresh = false;
+      if (hl == 0) slots[sx].n_memo = 0;
+#ifdef PG_TIMELINE  // experiment build: per-game wall-clock start/end into p.trace
+      t_start = wall_clock64();
+#endif
     }
     const int s1b = st.s1, s2b = st.s2;
     const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
@@ -703,10 +904,8 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
       // right side: [bx, by, lbx, lby, me=right, enemy=left]; left side x-flipped (main.py:146-147)
       const int k[6] = {side ? 320 - bx2 : bx2, by2, side ? 320 - lbx2 : lbx2, lby2, side ? lc2 : rc2,
                         side ? rc2 : lc2};
-      float x[6], acc[O], z[O];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) x[i] = feat32(k[i]);
-      partial_f32<U, O>(net, x, acc);
+      float acc[O], z[O];
+      partial_pk<U, O>(net, k, acc);
 #pragma unroll
       for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
       int idx = certify<O>(z, net.e);
@@ -715,19 +914,41 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
 #ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
       if (idx < 0) idx = z[1] > z[0] ? 1 : 0;
 #endif
-      if (idx < 0) {  // rare, half-uniform: ask the service wave for the f64 decision
-        if (hl == 0) {
-          slot->g = gm;
+      if (idx < 0) {  // rare, half-uniform: the memo, else ask the service wave
+        fails += 1;
+        const uint64_t key = memo_key(k);
+        const int nm = slots[sx].n_memo;
+        int hit = -1;
+#pragma unroll 1
+        for (int c = 0; c < kMemo && c < nm; ++c)
+          if (slots[sx].memo_key[c] == key) hit = slots[sx].memo_idx[c];
+        if (hit != -1) {
+          idx = hit;
+        } else {
+          if (hl == 0) {
+            slots[sx].g = gm;
 #pragma unroll
-          for (int i = 0; i < 6; ++i) slot->k[i] = k[i];
+            for (int i = 0; i < 6; ++i) slots[sx].k[i] = k[i];
+#pragma unroll
+            for (int o = 0; o < O; ++o) slots[sx].z[o] = z[o];
+            slots[sx].e = net.e;
+            __threadfence_block();
+            slots[sx].flag = 1;
+          }
+          while (slots[sx].flag != 2) __builtin_amdgcn_s_sleep(1);
           __threadfence_block();
-          slot->flag = 1;
+          const int ans = slots[sx].idx;
+          slow += (ans >> 8) & 1;
+          plateau += ans >> 9;
+          idx = ans & 255;
+          if (hl == 0) {
+            const int c = nm % kMemo;  // round-robin replacement
+            slots[sx].memo_key[c] = key;
+            slots[sx].memo_idx[c] = idx;
+            slots[sx].n_memo = nm + 1;
+            slots[sx].flag = 0;
+          }
         }
-        while (slot->flag != 2) __builtin_amdgcn_s_sleep(1);
-        __threadfence_block();
-        idx = slot->idx;
-        if (hl == 0) slot->flag = 0;
-        slow += 1;
       }
       const int mine = index_to_code(idx);
       const int other = other_half<L>(mine);
@@ -739,8 +960,10 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
     }
     act_l = clamp_action(lc2, left);
     act_r = clamp_action(rc2, right);
+#ifndef PG_TIMELINE
     if (p.trace && w < p.trace_games && frames <= p.trace_cap && lig == 0)
       p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+#endif
     if (frames > 1) {
       if (st.s1 == s1b && st.s2 == s2b) {
         timeout += 1;
@@ -751,6 +974,15 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
     }
     if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
       if (lig == 0) finish_game(p, w, st, frames, total);
+#ifdef PG_TIMELINE
+      if (p.trace && w < p.trace_games && lig == 0) {
+        uint32_t *tl = (uint32_t *)(p.trace + (long)w * p.trace_cap);
+        tl[0] = (uint32_t)t_start;
+        tl[1] = (uint32_t)wall_clock64();
+        tl[2] = blockIdx.x;
+        tl[3] = threadIdx.x;
+      }
+#endif
       c_steps += frames;
       c_games += 1;
       int ww = 0;
@@ -766,6 +998,8 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(EvalParams p) {
       atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
     }
     if (hl == 0 && slow) atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
+    if (hl == 0 && fails) atomicAdd((unsigned long long *)&p.counters[4], (unsigned long long)fails);
+    if (hl == 0 && plateau) atomicAdd((unsigned long long *)&p.counters[5], (unsigned long long)plateau);
   }
   // this wave will post no more requests
   if (lane64 == 0) atomicAdd(&waves_done, 1);
@@ -1087,18 +1321,21 @@ static int32_t launch_resident(const EvalParams &p, hipStream_t s) {
   return PG_OK;
 }
 
-// split layout for hidden width H: L lanes per game (L/2 per network) with
-// the fewest units per lane that keep the group within L/2 lanes of work
+// split layout for hidden width H: L lanes per game (L/2 per network).  Fewer
+// lanes per game means more games per wave, so the replicated scalar work of
+// a frame (physics, bookkeeping, the certificate) is shared by fewer lanes;
+// L = 8 holds up to 16 units per lane (H <= 64) in 256 VGPRs (measured
+// fastest for [6,64,3]: profiles/r01/sweep_lanes.log).
 static int choose_split_lanes(int H) {
-  if (H <= 4) return 8;
-  if (H <= 16) return 16;
-  if (H <= 64) return 32;
+  if (H <= 64) return 8;
+  if (H <= 128) return 32;
   return 64;
 }
 
 template <int L, int U, int O, typename WT>
 static int32_t launch_service(const EvalParams &p, hipStream_t s) {
-  constexpr int GPB = kSvcGameWaves * (64 / L);  // game groups per block
+  constexpr int kSvcThreads = svc_threads<U>();
+  constexpr int GPB = (kSvcThreads / 64 - 1) * (64 / L);  // game groups per block
   const size_t lds = (size_t)f64_lds_doubles(p.nodes[1], O) * sizeof(double);
   const int want = (p.total + GPB - 1) / GPB;
   const int cap = num_cus() * 2;
@@ -1118,7 +1355,7 @@ static int32_t launch_service_any(const EvalParams &p, int L, int O, hipStream_t
     if (O == 3) return launch_service<LL, UU, 3, WT>(p, s);              \
     if (O == 4) return launch_service<LL, UU, 4, WT>(p, s);              \
   }
-  PG_SVC(8, 1) PG_SVC(8, 2) PG_SVC(16, 1) PG_SVC(16, 2) PG_SVC(16, 4) PG_SVC(16, 8)
+  PG_SVC(8, 1) PG_SVC(8, 2) PG_SVC(8, 4) PG_SVC(8, 8) PG_SVC(8, 16) PG_SVC(16, 1) PG_SVC(16, 2) PG_SVC(16, 4) PG_SVC(16, 8)
   PG_SVC(32, 1) PG_SVC(32, 2) PG_SVC(32, 4) PG_SVC(32, 8) PG_SVC(64, 1) PG_SVC(64, 2) PG_SVC(64, 4) PG_SVC(64, 8)
 #undef PG_SVC
   return fail(PG_ERR_UNSUPPORTED, "no service kernel for L=%d H=%d O=%d", L, H, O);

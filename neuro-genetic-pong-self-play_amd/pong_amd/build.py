@@ -9,7 +9,8 @@ import sys
 from ._lib import LIB_PATH, PKG_DIR, REPO_DIR
 
 SOURCES = [os.path.join(PKG_DIR, "csrc", "pong_ga.hip")]
-DEPS = SOURCES + [os.path.join(PKG_DIR, "csrc", "pg_device.hpp"), os.path.join(REPO_DIR, "include", "pong_ga.h")]
+DEPS = SOURCES + [os.path.abspath(__file__), os.path.join(PKG_DIR, "csrc", "pg_device.hpp"), os.path.join(PKG_DIR, "csrc", "pg_f64math.h"),
+        os.path.join(REPO_DIR, "include", "pong_ga.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PG_OFFLOAD_ARCH", "gfx950")
 
@@ -24,7 +25,10 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB_PATH
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
+           # no SLP packing of independent f32 adds into v_pk_add_f32: it breaks the
+           # DPP-fused reductions into mov_dpp + pk_add pairs (measured -5 %)
+           "-fno-slp-vectorize", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO_DIR, "include"),
            "-o", LIB_PATH + ".tmp"] + SOURCES
     if verbose:

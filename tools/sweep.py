@@ -24,7 +24,7 @@ def one(args):
     dev = torch.device("cuda", 0)
     shape = [int(v) for v in args.shape.split(",")]
     n, H = args.pop, args.pop // 4
-    ev = Evaluator(shape, device=dev, group_lanes=args.lane, kernel="resident",
+    ev = Evaluator(shape, device=dev, group_lanes=args.lane, kernel=args.kernel,
                    dtype=torch.float64 if args.dtype == "f64" else torch.float32)
     gen = torch.Generator(device=dev).manual_seed(1234)
     genomes = (torch.randn((n, ev.genes), generator=gen, dtype=torch.float64, device=dev) * args.sigma).to(ev.dtype)
@@ -41,11 +41,13 @@ def one(args):
         torch.cuda.synchronize()
         ms.append(a.elapsed_time(b))
         c = res.counters.cpu()
-        steps, fwd, slow = int(c[0]), int(c[1]), int(c[2])
+        steps, fwd, slow, fails, plateau = int(c[0]), int(c[1]), int(c[2]), int(c[4]), int(c[5])
     mean = sum(ms) / len(ms)
     print(json.dumps({"lib": os.path.basename(os.environ.get("PONG_GA_LIB", "default")), "lanes": args.lane,
+                      "kernel": args.kernel,
                       "shape": shape, "kernel_ms": mean, "min_ms": min(ms), "env_steps": steps,
-                      "env_steps_per_s": steps / (mean / 1e3), "fwd": fwd, "f64_redecide": slow}), flush=True)
+                      "env_steps_per_s": steps / (mean / 1e3), "fwd": fwd, "f64_redecide": slow,
+                      "cert_fail": fails, "plateau": plateau, "memo_hits": fails - plateau - slow}), flush=True)
 
 
 def main():
@@ -57,6 +59,7 @@ def main():
     p.add_argument("--shape", default="6,64,3")
     p.add_argument("--sigma", type=float, default=3.0)
     p.add_argument("--dtype", default="f64")
+    p.add_argument("--kernel", default="split")
     p.add_argument("--one", action="store_true")
     p.add_argument("--lane", type=int, default=0)
     args = p.parse_args()
@@ -69,7 +72,8 @@ def main():
             if lib:
                 env["PONG_GA_LIB"] = os.path.abspath(lib)
             cmd = [sys.executable, __file__, "--one", f"--lane={lane}", "--reps", str(args.reps),
-                   "--pop", str(args.pop), "--shape", args.shape, "--sigma", str(args.sigma), "--dtype", args.dtype]
+                   "--pop", str(args.pop), "--shape", args.shape, "--sigma", str(args.sigma), "--dtype", args.dtype,
+                   "--kernel", args.kernel]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 print(json.dumps({"lib": lib, "lanes": lane, "error": r.stderr[-800:]}), flush=True)
