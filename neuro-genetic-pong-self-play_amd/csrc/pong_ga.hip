@@ -738,7 +738,53 @@ struct SlowSlot {
   volatile int memo_idx[kMemo];
 };
 
-// Plateau certificate, tried by the service wave before a full f64 forward.
+// The plateau certificate in f32, tried by the game wave itself where
+// certify() failed (no round trip to the service wave).  Same rule as
+// plateau_decide below, but m(z) = rint(2^52 pow(e, -z)) is only bracketed:
+// v = exp2(52 - z log2 e) in f32 is within 2e-5 v of 2^52 e^-z (exponent
+// rounding <= (|t| + 2 |z| log2 e) u, v_exp_f32 ~1 ulp, x4 margin), so
+// ceil(v(z + e) - d - 1/2) <= m_true <= floor(v(z - e) + d + 1/2).  Useful
+// where v is small (z >~ 28); near 22 the bracket is wide and the service
+// decides.
+template <int O>
+__device__ __forceinline__ int plateau_f32(const float z[O], float e) {
+  constexpr int kBelow = 0x7ffffff0;  // S below the plateau regime (z < 22)
+  constexpr int kNone = 0x7fffffff;   // cannot bracket
+  int mlo[O], mhi[O];
+  bool bad = false;
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    const float zl = z[o] - e, zh = z[o] + e;
+    bad = bad || !(zl == zl);  // NaN
+    // upper bracket of m from the low end z - e (valid when z - e >= 22.2)
+    if (zl >= 22.2f) {
+      const float v = __builtin_amdgcn_exp2f(fmaf(-zl, 1.44269504f, 52.f));
+      mhi[o] = (int)floorf(v * (1.f + 2e-5f) + 0.5f);
+    } else {
+      mhi[o] = kNone;
+    }
+    // lower bracket of m from the high end z + e
+    if (zh >= 22.2f) {
+      const float v = __builtin_amdgcn_exp2f(fmaf(-zh, 1.44269504f, 52.f));
+      mlo[o] = (int)ceilf(v * (1.f - 2e-5f) - 0.5f);
+    } else {
+      mlo[o] = zh < 22.0f ? kBelow : -1;  // -1: straddles the regime edge, never "surely below"
+    }
+  }
+  if (bad) return -1;
+  int res = -1;
+#pragma unroll
+  for (int w = O - 1; w >= 0; --w) {
+    bool ok = mhi[w] != kNone;
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+      if (o != w) ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
+    res = ok ? w : res;
+  }
+  return res;
+}
+
+// Plateau certificate, tried first by the service wave (no memory traffic).
 // For z >= 22.2, numpy's S(z) = 1/(1 + pow(e, -z)) is exactly
 // 1 - m(z) 2^-52 with m(z) = rint(2^52 pow(e, -z)) (1 + p rounds to
 // 1 + m 2^-52; its reciprocal rounds to 1 - m 2^-52 while m < 2^20), so two
@@ -779,6 +825,139 @@ __device__ int plateau_decide(const float *z, float e, int lane) {
 #pragma unroll
     for (int o = 0; o < O; ++o)
       if (o != w) ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
+    if (ok) return w;
+  }
+  return -1;
+}
+
+// Certified f64 decision, tried by the service wave before the numpy-order
+// f64 forward.  The wave evaluates the network in f64 in parallel (one hidden
+// unit per lane, tree sums) and bounds its distance to numpy's own f64 result
+// z_np (numpy_nn.py:120-131: sequential dot products, bias last):
+//   |z - z_np| <= e_o = 2 eps (sum_j |W2_oj| (4 A_j + 84) + 2 |c_o|),
+// eps = 2^-53, A_j = sum_i |W1_ji x_i| + |b_j| -- both dot products within
+// gamma_7 A_j of the exact one, slope <= 1/4, both sigmoids within 6 ulp,
+// both output sums within gamma_66 + gamma_8 of exact, x2 margin.  That is
+// ~1e-11, ten orders below the f32 bound, so the decision is almost always
+// provable; with O outputs on lanes:
+//  * for z >= 22.2, S_np(z) = 1 - m(z) 2^-52 exactly, m(z) = rint(2^52
+//    pow(e, -z)) (1 + p rounds to 1 + m 2^-52, whose reciprocal rounds to
+//    1 - m 2^-52 while m < 2^20); m is monotone, so [z - e, z + e] bounds m
+//    between m(z + e) and m(z - e); ties are equal m, larger S is smaller m;
+//  * below that, S is strictly increasing on gaps above the plateau width
+//    4 2^-52 (e^z + 1), so a gap test decides.
+// Returns -1 when undecided (NaN, a rounding boundary within 1e-6 of m's
+// half-integer, or a tie the intervals cannot settle).
+// Sum of a double over the 64 lanes (DPP within rows, permlane swaps across).
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#define PG_DPP64(CTRL)                                                                          \
+  {                                                                                           \
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);                                  \
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)bits, CTRL, 0xF, 0xF, false); \
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(bits >> 32), CTRL, 0xF, 0xF, false); \
+    v += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));                        \
+  }
+  PG_DPP64(0xB1) PG_DPP64(0x4E) PG_DPP64(0x141) PG_DPP64(0x140)
+#undef PG_DPP64
+  {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)bits, (uint32_t)bits, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(bits >> 32), (uint32_t)(bits >> 32), false, false);
+    v = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0])) +
+        __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+  }
+  {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)bits, (uint32_t)bits, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(bits >> 32), (uint32_t)(bits >> 32), false, false);
+    v = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0])) +
+        __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+  }
+  return v;
+}
+
+template <int O, typename WT>
+__device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int *k, int lane) {
+  constexpr double kEps = 1.1102230246251565e-16;  // 2^-53
+  double x[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
+  const int cols = 6 + b;
+  const WT *v = g + (long)H * cols;
+  double zp[O], ep[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) { zp[o] = 0.0; ep[o] = 0.0; }
+#pragma unroll 1
+  for (int j = lane; j < H; j += 64) {
+    const WT *row = g + (long)j * cols;
+    double a = b ? (double)row[6] : 0.0;
+    double A = fabs(a);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double w = (double)row[i];
+      a = fma(w, x[i], a);
+      A = fma(fabs(w), x[i], A);
+    }
+    const double sj = pg_sigmoid_f64(a);
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      const double w2 = (double)v[(long)o * (H + b) + j];
+      zp[o] = fma(w2, sj, zp[o]);
+      ep[o] = fma(fabs(w2), 4.0 * A + 84.0, ep[o]);
+    }
+  }
+  double z[O], e[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    const double t = wave_sum_f64(zp[o]);  // any order: e covers it
+    const double u = wave_sum_f64(ep[o]);
+    const double c = b ? (double)v[(long)o * (H + b) + H] : 0.0;
+    z[o] = t + c;
+    e[o] = 2.0 * kEps * (u + 2.0 * fabs(c)) * 1.001 + 1e-300;
+  }
+  // m-intervals: lanes 0..2O-1 each evaluate one endpoint (z -/+ e)
+  constexpr int kBig = 0x7fffffff;  // below the plateau regime
+  int m = kBig;
+  bool amb = false;
+  if (lane < 2 * O) {
+    double zo = z[0], eo = e[0];
+#pragma unroll
+    for (int o = 1; o < O; ++o)
+      if ((lane >> 1) == o) { zo = z[o]; eo = e[o]; }
+    const double zz = (lane & 1) ? zo + eo : zo - eo;
+    if (zz != zz) {
+      amb = true;  // NaN: numpy's NaN rule, in the full path
+    } else if (zz >= 22.2) {
+      double t = pg_exp_f64(-zz);
+      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z), as pg_sigmoid_f64
+      const double vv = t * 4503599627370496.0;   // 2^52 p
+      amb = fabs(vv - floor(vv) - 0.5) < 1e-6;
+      m = (int)rint(vv);
+    } else if (zz >= 22.0) {
+      amb = true;  // too close to the regime edge to compare across it
+    }
+  }
+  if (__ballot(amb)) return -1;
+  int mlo[O], mhi[O];  // m(z + e) <= m_np <= m(z - e)
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    mhi[o] = __builtin_amdgcn_readlane(m, 2 * o);
+    mlo[o] = __builtin_amdgcn_readlane(m, 2 * o + 1);
+  }
+#pragma unroll
+  for (int w = 0; w < O; ++w) {
+    bool ok = true;
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      if (o == w) continue;
+      if (mhi[w] != kBig) {  // w surely in the plateau regime
+        ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
+      } else {  // S_w below the regime: a strict gap above the plateau width
+        const double top = z[w] + e[w];
+        const double tw = 8.881784197001252e-16 * (pg_exp_f64(fmin(top, 40.0)) + 1.0);
+        ok = ok && (z[w] - e[w] > z[o] + e[o] + tw);
+      }
+    }
     if (ok) return w;
   }
   return -1;
@@ -825,11 +1004,12 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           int k[6];
 #pragma unroll
           for (int i = 0; i < 6; ++i) k[i] = slots[sl].k[i];
-          float z[O];
+          float zf[O];
 #pragma unroll
-          for (int o = 0; o < O; ++o) z[o] = slots[sl].z[o];
-          int idx = plateau_decide<O>(z, slots[sl].e, lane64);
-          // bit 8 / bit 9 of the answer: decided by a full f64 forward / by the plateau rule
+          for (int o = 0; o < O; ++o) zf[o] = slots[sl].z[o];
+          int idx = plateau_decide<O>(zf, slots[sl].e, lane64);
+          if (idx < 0) idx = fast_f64_decide<O, WT>(g, H, b, k, lane64);
+          // bit 8 / bit 9 of the answer: decided by the numpy-order forward / by the certified one
           idx = idx < 0 ? (256 | forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64))
                         : (512 | idx);
           if (lane64 == 0) {
@@ -863,7 +1043,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   Pong st;
   int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
   const WT *gm = genomes;
-  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0;
+  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0;
 
   int w;
   {
@@ -874,6 +1054,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   bool fresh = true;
 #ifdef PG_TIMELINE
   uint64_t t_start = 0;
+  uint32_t g_fails = 0, g_slow = 0;
 #endif
   while (w < p.total) {
     if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
@@ -889,6 +1070,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       if (hl == 0) slots[sx].n_memo = 0;
 #ifdef PG_TIMELINE  // experiment build: per-game wall-clock start/end into p.trace
       t_start = wall_clock64();
+      g_fails = g_slow = 0;
 #endif
     }
     const int s1b = st.s1, s2b = st.s2;
@@ -916,6 +1098,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #endif
       if (idx < 0) {  // rare, half-uniform: the memo, else ask the service wave
         fails += 1;
+#ifdef PG_TIMELINE
+        g_fails += 1;
+#endif
+        idx = plateau_f32<O>(z, net.e);
+        inwave += idx >= 0 ? 1 : 0;
+      }
+      if (idx < 0) {
         const uint64_t key = memo_key(k);
         const int nm = slots[sx].n_memo;
         int hit = -1;
@@ -939,6 +1128,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           __threadfence_block();
           const int ans = slots[sx].idx;
           slow += (ans >> 8) & 1;
+#ifdef PG_TIMELINE
+          g_slow += 1;  // service round trips
+#endif
           plateau += ans >> 9;
           idx = ans & 255;
           if (hl == 0) {
@@ -979,8 +1171,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         uint32_t *tl = (uint32_t *)(p.trace + (long)w * p.trace_cap);
         tl[0] = (uint32_t)t_start;
         tl[1] = (uint32_t)wall_clock64();
-        tl[2] = blockIdx.x;
-        tl[3] = threadIdx.x;
+        tl[2] = g_fails;
+        tl[3] = g_slow;
       }
 #endif
       c_steps += frames;
@@ -1000,6 +1192,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     if (hl == 0 && slow) atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
     if (hl == 0 && fails) atomicAdd((unsigned long long *)&p.counters[4], (unsigned long long)fails);
     if (hl == 0 && plateau) atomicAdd((unsigned long long *)&p.counters[5], (unsigned long long)plateau);
+    if (hl == 0 && inwave) atomicAdd((unsigned long long *)&p.counters[6], (unsigned long long)inwave);
   }
   // this wave will post no more requests
   if (lane64 == 0) atomicAdd(&waves_done, 1);

@@ -55,8 +55,9 @@ class EvalResult:
     frames: torch.Tensor        # [n, games] int32 env steps
     total_frames: torch.Tensor  # [n, games] f64
     status: torch.Tensor        # [n] int32, 1 = ZeroDivisionError
-    counters: torch.Tensor      # [6] int64: env steps, NN forwards, full f64 forwards, games,
-    #                             certificate failures, failures decided by the plateau rule
+    counters: torch.Tensor      # [8] int64: env steps, NN forwards, numpy-order f64 forwards, games,
+    #                             certificate failures, decided by the service's certified f64 rules,
+    #                             decided in-wave by the f32 plateau rule, 0
 
 
 class Evaluator:
@@ -138,7 +139,7 @@ class Evaluator:
                 frames=torch.empty((n, games), dtype=torch.int32, device=dev),
                 total_frames=torch.empty((n, games), dtype=torch.float64, device=dev),
                 status=torch.empty(n, dtype=torch.int32, device=dev),
-                counters=torch.zeros(6, dtype=torch.int64, device=dev))
+                counters=torch.zeros(8, dtype=torch.int64, device=dev))
         else:
             out.counters.zero_()
         trace = None

@@ -205,8 +205,8 @@ def test_eval_near_saturation_matches_oracle(gpu, oracle):
     res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
     _assert_same(res, ref)
     c = res.counters.cpu().numpy()
-    assert c[4] > 0 and c[5] > 0, c          # the plateau rule was exercised
-    assert c[2] + c[5] <= c[4], c            # full f64 + plateau <= certificate failures
+    assert c[4] > 0 and c[5] > 0 and c[6] > 0, c    # in-wave and service certificates both exercised
+    assert c[2] + c[5] + c[6] <= c[4], c           # each failure is decided once
 
 
 def test_eval_f32_genomes(gpu, oracle):

@@ -41,13 +41,14 @@ def one(args):
         torch.cuda.synchronize()
         ms.append(a.elapsed_time(b))
         c = res.counters.cpu()
-        steps, fwd, slow, fails, plateau = int(c[0]), int(c[1]), int(c[2]), int(c[4]), int(c[5])
+        steps, fwd, slow, fails, plateau, tight = int(c[0]), int(c[1]), int(c[2]), int(c[4]), int(c[5]), int(c[6])
     mean = sum(ms) / len(ms)
     print(json.dumps({"lib": os.path.basename(os.environ.get("PONG_GA_LIB", "default")), "lanes": args.lane,
                       "kernel": args.kernel,
                       "shape": shape, "kernel_ms": mean, "min_ms": min(ms), "env_steps": steps,
                       "env_steps_per_s": steps / (mean / 1e3), "fwd": fwd, "f64_redecide": slow,
-                      "cert_fail": fails, "plateau": plateau, "memo_hits": fails - plateau - slow}), flush=True)
+                      "cert_fail": fails, "inwave_plateau": tight, "service_certified": plateau,
+                      "memo_hits": fails - tight - plateau - slow}), flush=True)
 
 
 def main():

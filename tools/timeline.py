@@ -56,11 +56,21 @@ def main():
     out["us_per_frame_long_median"] = float(np.median(dur[long] / frames[long]))
     last = np.argsort(end)[-5:]
     out["last_games"] = [{"frames": int(frames[i]), "start": float(start[i]), "end": float(end[i])} for i in last]
+    fails, trips = tl[:, 2], tl[:, 3]
+    out["fails_per_game_long_median"] = float(np.median(fails[long]))
+    out["trips_per_frame_last"] = [float(trips[i] / max(frames[i], 1)) for i in last]
+    # per-frame time vs service round trips per frame (games of > 500 frames)
+    m = frames > 500
+    if m.sum() > 10:
+        A = np.stack([np.ones(m.sum()), trips[m] / frames[m]], 1)
+        coef, *_ = np.linalg.lstsq(A, dur[m] / frames[m], rcond=None)
+        out["fit_us_per_frame"] = float(coef[0])
+        out["fit_us_per_trip"] = float(coef[1])
     grid = np.linspace(0, span, 21)
     out["running_games"] = [int(((start <= t) & (end > t)).sum()) for t in grid]
     print(json.dumps(out), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
-    np.savez_compressed(args.out, start=start, end=end, frames=frames, block=tl[:, 2], thread=tl[:, 3])
+    np.savez_compressed(args.out, start=start, end=end, frames=frames, fails=tl[:, 2], trips=tl[:, 3])
 
 
 if __name__ == "__main__":
