@@ -129,6 +129,7 @@ def main():
     steps_local = 0
     fwd_local = 0
     slow_local = 0
+    cert_local = [0, 0, 0]  # certificate failures, decided by the service wave, decided in-wave
     kernel_ms = []
     counters = []
     for s in range(args.steps):
@@ -148,9 +149,11 @@ def main():
         steps_local += int(c[0])
         fwd_local += int(c[1])
         slow_local += int(c[2])
+        for i in range(3):
+            cert_local[i] += int(c[4 + i])
 
-    t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)],
-                     dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)]
+                     + [float(v) for v in cert_local], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
@@ -159,9 +162,11 @@ def main():
         elapsed = float(tmax[0])
         steps_all, fwd_all, slow_all = float(tsum[1]), float(tsum[2]), float(tsum[3])
         kernel_ms_mean = float(tsum[4]) / world / args.steps
+        cert_all = [float(v) for v in tsum[5:8]]
     else:
         steps_all, fwd_all, slow_all = float(t[1]), float(t[2]), float(t[3])
         kernel_ms_mean = float(t[4]) / args.steps
+        cert_all = [float(v) for v in t[5:8]]
 
     if rank == 0:
         env_steps_per_s = steps_all / elapsed
@@ -192,11 +197,20 @@ def main():
                        "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                        "parallelism": f"dp{world}" if world > 1 else "dp1",
                        "env_steps_per_generation": steps_all / args.steps,
-                       "f64_redecisions_per_forward": slow_all / max(fwd_all, 1.0)},
-            "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
+                       "certificate_failures_per_forward": cert_all[0] / max(fwd_all, 1.0),
+                       "failures_decided_in_wave": cert_all[2] / max(cert_all[0], 1.0),
+                       "failures_decided_by_service_f64_certificate": cert_all[1] / max(cert_all[0], 1.0),
+                       "numpy_order_f64_forwards_per_forward": slow_all / max(fwd_all, 1.0)},
+            "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / F32_VECTOR_PEAK_TFLOPS,
-                         "traffic": None,
-                         "kernel": "k_service (pg_eval_population, split lanes + f64 service wave)",
+                         "traffic": _pmc_traffic(),
+                         "traffic_note": "HBM-side bytes per launch, rocprofv3 FETCH_SIZE + WRITE_SIZE of the "
+                                         "same command (profiles/r01/pmc_traffic.json, separate --pmc passes); "
+                                         "genome rows are re-read per game, the unique set is ~0.42 GB",
+                         "engine": "compute-bound on the f32 vector ALU (v_pk_fma_f32, v_exp_f32, v_rcp_f32); "
+                                   "peak = MI355X f32 dense peak, identical for VALU and MFMA (157.3 TF)",
+                         "kernel": "k_service<8,16,3,double> (pg_eval_population: 8 games per wave, "
+                                   "4 lanes per network, f64 service wave per block)",
                          "kernel_ms_per_launch": kernel_ms_mean,
                          "flops_per_forward": flops_per_forward,
                          "forwards_per_launch": fwd_per_launch,
@@ -232,6 +246,14 @@ def cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo):
             "sample": f"{done} genomes x {args.games} games of the same self-play workload "
                       f"({steps} env-steps in {dt:.1f} s, OpenMP over {args.cpu_threads} host threads)",
             "cpu": _cpu_model()}
+
+
+def _pmc_traffic():
+    try:
+        with open(os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")) as fh:
+            return json.load(fh)["traffic_bytes"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def _cpu_model():

@@ -14,7 +14,7 @@ timeout -k 10 400 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench exit=$rc" >> "$OUT/summary.txt"; fatal $rc bench
 ROOT=$(pwd)
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o kt --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o kt --output-format csv -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline "$@" > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof exit=$rc" >> "$OUT/summary.txt"; fatal $rc rocprof
 if [ -n "$PMC" ]; then
   for ctr in FETCH_SIZE WRITE_SIZE; do

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Per-launch memory traffic of the evaluation kernel from rocprofv3 PMC runs.
+
+Reads the FETCH_SIZE and WRITE_SIZE passes of tools/gpu_check.sh (PMC=1) and
+writes a JSON summary that bench.py reports as roofline.traffic.  FETCH_SIZE /
+WRITE_SIZE are in KiB per dispatch and count the L2's memory-side requests
+(Infinity-Cache hits included); MI355X_MICROARCH.md: FETCH_SIZE reads half the
+bytes of 16-B-per-lane streaming loads -- the genome loads here are 8-B
+scattered per-lane loads, a width the guide leaves uncalibrated, so the raw
+value is reported beside the x2 upper reading.
+usage: python tools/pmc_traffic.py gpurun_out/r16 profiles/r01/pmc_traffic.json
+"""
+import csv
+import json
+import sys
+
+
+def mean_counter(path, name):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if "k_service" in r["Kernel_Name"] and r["Counter_Name"] == name]
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    run, out = sys.argv[1], sys.argv[2]
+    fetch, nf = mean_counter(f"{run}/pmc_FETCH_SIZE/pmc_counter_collection.csv", "FETCH_SIZE")
+    write, nw = mean_counter(f"{run}/pmc_WRITE_SIZE/pmc_counter_collection.csv", "WRITE_SIZE")
+    kib = 1024.0
+    res = {"kernel": "k_service", "dispatches": [nf, nw],
+           "fetch_bytes_raw": fetch * kib, "write_bytes": write * kib,
+           "traffic_bytes": (fetch + write) * kib,
+           "traffic_bytes_fetch_x2": (2 * fetch + write) * kib,
+           "source": run}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
