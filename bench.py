@@ -81,11 +81,14 @@ def main():
                      group_lanes=args.group_lanes)
     G = ev.genes
 
-    # replicated population (identical on every rank: same seed), HoF = first H genomes
+    # replicated population (identical on every rank: same seed), HoF = first H genomes.
+    # Storage [H + P, G]: rows [0, H) the hall of fame, rows [H, H + P) the
+    # population, so the HoF candidates (HoF + population) are one gather.
     gen = torch.Generator(device=dev).manual_seed(args.seed)
-    pop = torch.randn((P, G), generator=gen, dtype=torch.float64, device=dev).mul_(args.sigma).to(dtype)
-    off = torch.empty_like(pop)
-    hof = pop[:H].clone()
+    store = torch.empty((H + P, G), dtype=dtype, device=dev)
+    store[H:] = torch.randn((P, G), generator=gen, dtype=torch.float64, device=dev).mul_(args.sigma).to(dtype)
+    store[:H] = store[H:H + H]
+    spare = torch.empty_like(store)
     hof_fit = torch.full((H,), -1e300, dtype=torch.float64, device=dev)
     lo, hi = PD.shard_range(P, rank, world)
     kind, opp, mult = ev.selfplay_schedule(hi - lo, H, offset=lo)
@@ -96,7 +99,8 @@ def main():
     ev_end = torch.cuda.Event(enable_timing=True)
 
     def generation(g, timed):
-        nonlocal pop, off, hof, hof_fit, res_buf
+        nonlocal store, spare, hof_fit, res_buf
+        hof, pop = store[:H], store[H:]
         if timed:
             ev_start.record()
         res, _ = ev.evaluate(pop[lo:hi], kind, opp, mult, opponents=hof, out=res_buf, validate=False)
@@ -104,19 +108,16 @@ def main():
             ev_end.record()
         res_buf = res
         fit = PD.gather_fitness(res.fitness, P) if world > 1 else res.fitness
-        # hall of fame: best H of (HoF, population)
+        # hall of fame: best H of (HoF, population), gathered into the next storage
         cand = torch.cat([hof_fit, fit])
         top = torch.topk(cand, H, sorted=False).indices
-        from_hof = top < H
-        new_hof = torch.empty_like(hof)
-        new_hof[from_hof] = hof[top[from_hof]]
-        new_hof[~from_hof] = pop[top[~from_hof] - H]
-        hof, hof_fit = new_hof, cand[top]
-        # selection + variation
+        torch.index_select(store, 0, top, out=spare[:H])
+        hof_fit = cand[top]
+        # selection + variation: offspring into the next storage's population rows
         chosen = D.select_tournament_ranked(fit, P, tournsize, seed=args.seed, generation=g)
-        off, _ = D.vary(pop, chosen, G, cxpb, mutpb, alpha, mu, sigma, indpb, seed=args.seed,
-                        generation=g, out=off)
-        pop, off = off, pop
+        D.vary(pop, chosen, G, cxpb, mutpb, alpha, mu, sigma, indpb, seed=args.seed,
+               generation=g, out=spare[H:])
+        store, spare = spare, store
         return res
 
     for w in range(args.warmup):
@@ -218,7 +219,7 @@ def main():
                          "streaming_equivalent_frac_of_hbm": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9 / HBM_PEAK_GBS},
         }
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo)
+            out["cpu_baseline"] = cpu_baseline(args, shape, store[H:], store[:H], kind, opp, mult, lo)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

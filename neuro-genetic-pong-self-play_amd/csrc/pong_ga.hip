@@ -421,15 +421,28 @@ __device__ __forceinline__ void partial_pk(const NetP<U, O> &n, const int k[6], 
   float2v a2[O];
 #pragma unroll
   for (int o = 0; o < O; ++o) a2[o] = float2v{0.f, 0.f};
+  // two unit pairs per step: their dependent pk_fma chains interleave, so the
+  // wait state a packed op owes its dependent successor is filled with work
 #pragma unroll
-  for (int p = 0; p < P; ++p) {
-    float2v a = n.w1[p][6];
+  for (int p = 0; p < P; p += 2) {
+    constexpr int kStep = 2;
+    const bool two = p + 1 < P;
+    float2v a = n.w1[p][6], b = two ? n.w1[p + 1][6] : float2v{0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 6; ++i) a = __builtin_elementwise_fma(n.w1[p][i], kx[i], a);
-    float2v q = float2v{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
-    const float2v sg = float2v{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+    for (int i = 0; i < 6; ++i) {
+      a = __builtin_elementwise_fma(n.w1[p][i], kx[i], a);
+      if (two) b = __builtin_elementwise_fma(n.w1[p + 1][i], kx[i], b);
+    }
+    const float2v qa = float2v{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
+    const float2v qb = float2v{__builtin_amdgcn_exp2f(b.x), __builtin_amdgcn_exp2f(b.y)} + 1.0f;
+    const float2v sa = float2v{__builtin_amdgcn_rcpf(qa.x), __builtin_amdgcn_rcpf(qa.y)};
+    const float2v sb = float2v{__builtin_amdgcn_rcpf(qb.x), __builtin_amdgcn_rcpf(qb.y)};
 #pragma unroll
-    for (int o = 0; o < O; ++o) a2[o] = __builtin_elementwise_fma(n.w2[p][o], sg, a2[o]);
+    for (int o = 0; o < O; ++o) {
+      a2[o] = __builtin_elementwise_fma(n.w2[p][o], sa, a2[o]);
+      if (two) a2[o] = __builtin_elementwise_fma(n.w2[p + 1][o], sb, a2[o]);
+    }
+    (void)kStep;
   }
 #pragma unroll
   for (int o = 0; o < O; ++o) acc[o] = a2[o].x + a2[o].y;
@@ -1401,6 +1414,20 @@ __global__ void k_select_ranked(pg_select_args a, const double *sorted, const in
 // (i-1, i) w.p. cxpb, then mutGaussian each individual w.p. mutpb.
 //   cxBlend:     gamma = (1 + 2 alpha) U - alpha; x1' = (1-gamma) x1 + gamma x2; x2' = gamma x1 + (1-gamma) x2
 //   mutGaussian: w.p. indpb per gene, x += N(mu, sigma)
+// Counter-based randoms: a key per (generation, stream, pair or individual),
+// then one splitmix64 per gene.  The two individuals of a pair share one
+// Box-Muller draw (r cos t, r sin t), in f32 (the noise is added in f64).
+__device__ __forceinline__ uint64_t rng_key(uint64_t seed, uint64_t gen, uint64_t stream, uint64_t a) {
+  const uint64_t k = splitmix64(seed + 0x9E3779B97F4A7C15ull * (gen + 1));
+  return splitmix64(k ^ (stream * 0xD6E8FEB86659FD93ull + a));
+}
+__device__ __forceinline__ double rng_u01(uint64_t key, uint64_t b) {
+  return (double)(splitmix64(key ^ b) >> 11) * 0x1.0p-53;
+}
+__device__ __forceinline__ float rng_u01f(uint64_t key, uint64_t b) {
+  return (float)(splitmix64(key ^ b) >> 40) * 0x1.0p-24f;
+}
+
 template <typename WT>
 __global__ void k_vary(pg_ga_args a) {
   const long gene = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1413,30 +1440,34 @@ __global__ void k_vary(pg_ga_args a) {
     const bool has1 = i1 < a.n;
     double x1 = (double)par[(long)a.chosen[i0] * a.stride + gene];
     double x2 = has1 ? (double)par[(long)a.chosen[i1] * a.stride + gene] : 0.0;
-    const bool cx = has1 && u01(a.seed, a.generation, 2, (uint64_t)pair, 0) < a.cxpb;
+    const bool cx = has1 && rng_u01(rng_key(a.seed, a.generation, 2, (uint64_t)pair), 0) < a.cxpb;
     if (cx) {
-      const double gamma =
-          __dadd_rn(__dmul_rn(1.0 + 2.0 * a.alpha, u01(a.seed, a.generation, 3, (uint64_t)pair, gene)), -a.alpha);
+      const double u = rng_u01(rng_key(a.seed, a.generation, 3, (uint64_t)pair), (uint64_t)gene);
+      const double gamma = __dadd_rn(__dmul_rn(1.0 + 2.0 * a.alpha, u), -a.alpha);
       const double y1 = __dadd_rn(__dmul_rn(1.0 - gamma, x1), __dmul_rn(gamma, x2));
       const double y2 = __dadd_rn(__dmul_rn(gamma, x1), __dmul_rn(1.0 - gamma, x2));
       x1 = y1;
       x2 = y2;
     }
-    bool mut[2] = {false, false};
-    double xs[2] = {x1, x2};
-    for (int s = 0; s < (has1 ? 2 : 1); ++s) {
-      const int ind = i0 + s;
-      mut[s] = u01(a.seed, a.generation, 4, (uint64_t)ind, 0) < a.mutpb;
-      if (mut[s] && u01(a.seed, a.generation, 5, (uint64_t)ind, gene) < a.indpb) {
-        // Box-Muller from two counter-based uniforms
-        const double u1 = 1.0 - u01(a.seed, a.generation, 6, (uint64_t)ind, gene);
-        const double u2 = u01(a.seed, a.generation, 7, (uint64_t)ind, gene);
-        const double nrm = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-        xs[s] = __dadd_rn(xs[s], __dadd_rn(a.mu, __dmul_rn(a.sigma, nrm)));
-      }
+    bool mut[2], hit[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint64_t ind = (uint64_t)(i0 + s);
+      mut[s] = (s == 0 || has1) && rng_u01(rng_key(a.seed, a.generation, 4, ind), 0) < a.mutpb;
+      hit[s] = mut[s] && rng_u01(rng_key(a.seed, a.generation, 5, ind), (uint64_t)gene) < a.indpb;
     }
-    off[(long)i0 * a.stride + gene] = (WT)xs[0];
-    if (has1) off[(long)i1 * a.stride + gene] = (WT)xs[1];
+    if (hit[0] || hit[1]) {
+      const uint64_t kb = rng_key(a.seed, a.generation, 6, (uint64_t)pair);
+      const float u1 = 1.0f - rng_u01f(kb, 2 * (uint64_t)gene);  // (0, 1]
+      const float u2 = rng_u01f(kb, 2 * (uint64_t)gene + 1);
+      const float r = sqrtf(-2.0f * logf(u1));
+      float sn, cs;
+      sincosf(6.2831853f * u2, &sn, &cs);
+      if (hit[0]) x1 = __dadd_rn(x1, __dadd_rn(a.mu, __dmul_rn(a.sigma, (double)(r * cs))));
+      if (hit[1]) x2 = __dadd_rn(x2, __dadd_rn(a.mu, __dmul_rn(a.sigma, (double)(r * sn))));
+    }
+    off[(long)i0 * a.stride + gene] = (WT)x1;
+    if (has1) off[(long)i1 * a.stride + gene] = (WT)x2;
     if (gene == 0) {
       a.invalid[i0] = (uint8_t)(cx || mut[0]);
       if (has1) a.invalid[i1] = (uint8_t)(cx || mut[1]);
