@@ -74,7 +74,10 @@ typedef enum pg_kernel {
   PG_KERNEL_GENERAL = 1,   /* one wave per game, f64, any NETWORK_SHAPE */
   PG_KERNEL_RESIDENT = 2,  /* [6, H<=256, 2..4]: one lane group holds both paddles' weights */
   PG_KERNEL_SPLIT = 3      /* [6, H<=256, 2..4]: half a lane group per paddle's network, plus one
-                              f64 service wave per 1024-thread block for re-decisions */
+                              f64 service wave per 1024-thread block for re-decisions */,
+  PG_KERNEL_WIDE = 4       /* [6, H1<=512, H2<=512, 1..4], n_games <= 8: one 512-thread workgroup per
+                              genome plays its games in lockstep and streams W2 from HBM each frame
+                              (numpy_nn's f64 order; AUTO picks it for H1 or H2 >= 64) */
 } pg_kernel;
 
 /* NETWORK_SHAPE (config.py:30-32) + BIAS (config.py:34) + genome storage type. */

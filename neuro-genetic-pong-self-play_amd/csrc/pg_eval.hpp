@@ -1,0 +1,87 @@
+// pg_eval.hpp -- what the evaluation kernels of libpong_ga.so share across
+// translation units (pong_ga.hip: the small-network kernels and the C-ABI;
+// pg_wide.hip: the streaming kernel for wide two-hidden-layer networks).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pong_ga.h"
+#include "pg_device.hpp"
+
+namespace pg {
+
+// Record a failure for pg_last_error() and return code (defined in pong_ga.hip).
+int32_t fail(int32_t code, const char *fmt, ...);
+
+#define PG_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(PG_ERR_HIP, "%s failed: %s", #call, hipGetErrorString(e_));        \
+  } while (0)
+
+// ------------------------------------------------------- kernel params ----
+struct EvalParams {
+  const void *genomes;
+  const void *opponents;
+  const int32_t *rows;  // unused (reserved)
+  const int32_t *kind;
+  const int32_t *opp;
+  const double *mult;
+  double *rewards;
+  int32_t *scores;
+  int32_t *frames;
+  double *total_frames;
+  int32_t *status_game;  // [n*games] scratch: zero-division per game
+  uint64_t *counters;
+  uint8_t *trace;
+  unsigned int *work;    // dynamic game counter (workspace)
+  int64_t gstride, ostride;
+  uint64_t seed;
+  int n_genomes, n_games, total;
+  int trace_games, trace_cap;
+  int nodes[PG_MAX_NODES];
+  int n_nodes, bias, max_width;
+};
+
+// Results of one finished game: perform_episode's return value and the
+// bookkeeping around it (main.py:108-112, utils.py:104-109).
+__device__ inline void finish_game(const EvalParams &p, int w, const Pong &st, int frames, int total) {
+  const double mult = p.mult[w];
+  double reward = 0.0;
+  int zero_div = 0;
+  if (st.s1 != st.s2) {
+    const double tf = (double)total;
+    if (tf == 0.0) {
+      zero_div = 1;
+      reward = __builtin_nan("");
+    } else {
+      // ((my - enemy) + my * mult) / (total_frames / 100.0), no contraction
+      const double diff = (double)(st.s2 - st.s1);
+      const double bonus = __dmul_rn((double)st.s2, mult);
+      reward = __dadd_rn(diff, bonus) / (tf / 100.0);
+    }
+  }
+  p.rewards[w] = reward;
+  p.scores[2 * w] = st.s1;
+  p.scores[2 * w + 1] = st.s2;
+  p.frames[w] = frames;
+  p.total_frames[w] = (double)total;
+  p.status_game[w] = zero_div;
+}
+
+// Features of utils.inference (utils.py:139-153) in f64 from doubled
+// centroids k: value = (k / 2) / 160, exactly the reference's rounding.
+__device__ inline double feat64(int k) { return __dmul_rn(0.5, (double)k) / 160.0; }
+__device__ inline double feat64_flip(int k) { return (160.0 - __dmul_rn(0.5, (double)k)) / 160.0; }
+
+
+int num_cus();
+
+// [6, H1, H2, O] networks (two hidden layers, H1, H2 <= 512, O in 2..4,
+// n_games <= 8) on the weight-streaming kernel k_wide (pg_wide.hip).
+bool wide_shape_ok(const pg_net &n, int n_games);
+int32_t launch_wide(const EvalParams &p, int dtype, hipStream_t s);
+
+}  // namespace pg

@@ -1,0 +1,391 @@
+// pg_wide.hip -- k_wide: evaluate() (main.py:28-66) for wide two-hidden-layer
+// networks [6, H1, H2, O] (BASELINE config 5: [6, 512, 512, 3], 267 779 genes).
+//
+// A wide network does not fit in registers (1 MB of f32 weights), so its
+// weights are STREAMED from HBM every frame.  One 512-thread workgroup per CU
+// plays all n_games (6) games of one genome in lockstep, so the genome's W2
+// (the 512 x 513 matrix that is 98 % of the genes) is read once per frame for
+// all six games; each NN opponent's W2 is read once per frame for its game.
+// Per frame:
+//   A  wave 0, one lane per game: physics step, centroids, features, the
+//      scripted left paddles; the set of networks that must run this frame
+//      (ball visible: get_actions main.py:143-153) goes to LDS.
+//   B  layer 1, thread j = hidden unit j, every needed column.
+//   C  layer 2: W2 tiles of 512 rows x K columns (128 B per row) pass
+//      HBM -> registers -> LDS (two tiles in flight per block), thread t owns
+//      row t and accumulates its dot product in k order; the genome's tile
+//      serves its six games' columns.
+//   D  layer 3: one thread per (column, output).
+//   E  wave 0: argmax, clamp, bookkeeping, termination, results.
+// Every dot product is numpy_nn's own operation sequence (numpy_nn.py:126-129:
+// W . [h; 1], a sequential f64 sum of f64 products, bias last) with the same
+// sigmoid as k_general, so k_wide and k_general agree bit for bit; the
+// streamed weights are exact (f32 or f64 genomes, widened to f64).
+#include <hip/hip_runtime.h>
+
+#include "pg_eval.hpp"
+
+namespace pg {
+
+constexpr int kWideThreads = 512;  // = max H2: one W2 row per thread
+constexpr int kWideMaxGames = 8;
+
+template <typename WT>
+struct WideTile;
+template <>
+struct WideTile<float> {
+  static constexpr int K = 32, KP = 33;  // 128 B of a row per tile; odd pitch: conflict-free row reads
+};
+template <>
+struct WideTile<double> {
+  static constexpr int K = 16, KP = 17;
+};
+
+// LDS carve (bytes): feats [NC][8] f64 | outputs [NC][4] f64 | control |
+// h1 [C2][NC] f64 | tile [512][KP] WT, reused for h2 [C3][NC] f64 after layer 2.
+constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffH1 = 2048;
+__host__ __device__ constexpr int align16(int v) { return (v + 15) & ~15; }
+
+__host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b, int wt_bytes, int KP) {
+  const int h1 = align16((H1 + b) * NC * 8);
+  const int tile = kWideThreads * KP * wt_bytes;
+  const int h2 = align16((H2 + b) * NC * 8);
+  return kOffH1 + h1 + (tile > h2 ? tile : h2);
+}
+
+// index of the q-th set bit of m (q < popcount(m))
+__device__ __forceinline__ int nth_set_bit(unsigned m, int q) {
+  for (int i = 0; i < q; ++i) m &= m - 1;
+  return __builtin_ctz(m);
+}
+
+// np.argmax over O activations: the first NaN if any, else the first maximum
+__device__ __forceinline__ int argmax_np(const double *v, int O) {
+  int best = 0;
+  for (int j = 1; j < O && !__builtin_isnan(v[best]); ++j)
+    if (__builtin_isnan(v[j]) || v[j] > v[best]) best = j;
+  return best;
+}
+
+template <int NG, typename WT>
+__global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  constexpr int NC = 2 * NG;  // columns: right (genome) of game c = c, left (opponent) of game c = NG + c
+  constexpr int K = WideTile<WT>::K, KP = WideTile<WT>::KP;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int b = p.bias;
+  const int H1 = p.nodes[1], H2 = p.nodes[2], O = p.nodes[3];
+  const int C1 = 6 + b, C2 = H1 + b, C3 = H2 + b;
+  const long W1n = (long)H1 * C1, W2n = (long)H2 * C2;
+  const int T = (C2 + K - 1) / K;  // tiles per W2
+
+  double *feat = (double *)lds_raw;              // [NC][8]
+  double *outv = (double *)(lds_raw + kOffOut);  // [NC][4]
+  int *ctl = (int *)(lds_raw + kOffCtl);         // [0] genome; frame-parity halves at [8..] and [40..]
+  long long *orow = (long long *)(lds_raw + kOffOrow);  // [NG] opponent row offsets (elements)
+  double *h1 = (double *)(lds_raw + kOffH1);            // [C2][NC]
+  WT *tile = (WT *)(lds_raw + kOffH1 + align16(C2 * NC * 8));
+  double *h2 = (double *)tile;  // [C3][NC], after layer 2
+
+  const WT *genomes = (const WT *)p.genomes;
+  const WT *opponents = (const WT *)p.opponents;
+  const int n_games = p.n_games;
+  uint64_t c_steps = 0, c_fwd = 0, c_games = 0, c_streams = 0;
+
+  for (;;) {  // genomes, one per workgroup at a time
+    if (t == 0) ctl[0] = (int)atomicAdd(p.work, 1u);
+    __syncthreads();
+    const int gi = ctl[0];
+    if (gi >= p.n_genomes) break;
+    const WT *gbase = genomes + (long)gi * p.gstride;
+
+    // game state: wave 0, lane g < n_games
+    Pong st;
+    int act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0, kind = 0, w = 0;
+    bool active = false;
+    if (wid == 0 && lane < n_games) {
+      w = gi * n_games + lane;
+      kind = p.kind[w];
+      orow[lane] = kind == kOppNN ? (long long)p.opp[w] * p.ostride : 0;
+      st.reset(game_seed(p.seed, lane), kind == kOppRomCpu);
+      active = true;
+    }
+    for (int fno = 0;; ++fno) {  // frames, all games in lockstep
+      int *cf = ctl + 8 + (fno & 1) * 32;  // [0] column mask, [1] any active, [2] nets, [3..] net ids
+      // ---- A: env.step + find_stuff + inference features (main.py:77-87)
+      int s1b = 0, s2b = 0, vis = 0, lc2 = 0, rc2 = 0, left = 0;
+      if (wid == 0) {
+        if (active) {
+          s1b = st.s1;
+          s2b = st.s2;
+          const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
+          st.step(act_r, act_l);
+          frames += 1;
+          vis = st.vis;
+          const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
+          lc2 = paddle_c2(st.lpy);
+          rc2 = paddle_c2(st.rpy);
+          if (vis) {  // get_actions main.py:143-150
+            const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
+            double *fr = feat + lane * 8;
+            fr[0] = feat64(bx2); fr[1] = feat64(by2); fr[2] = feat64(lbx2);
+            fr[3] = feat64(lby2); fr[4] = feat64(rc2); fr[5] = feat64(lc2); fr[6] = 1.0;
+            if (kind == kOppNN) {
+              double *fl = feat + (NG + lane) * 8;
+              fl[0] = feat64_flip(bx2); fl[1] = feat64(by2); fl[2] = feat64_flip(lbx2);
+              fl[3] = feat64(lby2); fl[4] = feat64(lc2); fl[5] = feat64(rc2); fl[6] = 1.0;
+            } else if (kind == kOppScore) {
+              left = (st.s1 <= st.s2) ? hardcoded(by2, lc2) : 0;
+            } else {
+              left = hardcoded(by2, lc2);
+            }
+          }
+        }
+        const uint64_t rb = __ballot(active && vis);
+        const uint64_t lb = __ballot(active && vis && kind == kOppNN);
+        const uint64_t ab = __ballot(active);
+        if (lane == 0) {
+          cf[0] = (int)((unsigned)rb | ((unsigned)lb << NG));
+          cf[1] = ab != 0;
+          int nn = 0;
+          if (rb) cf[3 + nn++] = 0;
+          for (int c = 0; c < NG; ++c)
+            if ((lb >> c) & 1) cf[3 + nn++] = 1 + c;
+          cf[2] = nn;
+        }
+      }
+      __syncthreads();
+      const unsigned mask = (unsigned)cf[0];
+      if (!cf[1]) break;
+      const int n_nets = cf[2];
+      c_streams += n_nets;  // uniform: every thread counts, thread 0 reports
+
+      if (mask) {
+        // ---- B: layer 1, h1 = S(W1 . [x; 1]) per needed column (numpy_nn.py:126-129)
+        for (int j = t; j < H1; j += kWideThreads) {
+          if (mask & ((1u << NG) - 1)) {
+            const WT *row = gbase + (long)j * C1;
+            double wv[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) wv[i] = (i < C1) ? (double)row[i] : 0.0;
+#pragma unroll
+            for (int c = 0; c < NG; ++c) {
+              if (!((mask >> c) & 1)) continue;
+              const double *x = feat + c * 8;
+              double z = 0.0;
+              for (int i = 0; i < C1; ++i) z = __dadd_rn(z, __dmul_rn(wv[i], x[i]));
+              h1[j * NC + c] = sigmoid_f64(z);
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < NG; ++c) {
+            if (!((mask >> (NG + c)) & 1)) continue;
+            const WT *row = opponents + orow[c] + (long)j * C1;
+            const double *x = feat + (NG + c) * 8;
+            double z = 0.0;
+            for (int i = 0; i < C1; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], x[i]));
+            h1[j * NC + NG + c] = sigmoid_f64(z);
+          }
+        }
+        if (b && t < NC) h1[H1 * NC + t] = 1.0;
+        __syncthreads();
+
+        // ---- C: layer 2, W2 streamed in tiles; thread t accumulates row t
+        double z[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) z[c] = 0.0;
+        double zo = 0.0;  // the current opponent network's row sum
+        const int S = n_nets * T;
+        // W2 rows through a buffer descriptor per network: the per-lane part of
+        // the offset is fixed (row t / K, column t % K of a tile), the rest is
+        // a scalar, so a tile's K loads cost no address registers; rows past
+        // H2 fall outside num_records and read 0.
+        const int lane_off = ((t / K) * C2 + (t % K)) * (int)sizeof(WT);
+        constexpr int kRowsPerLoad = kWideThreads / K;
+        auto net_rsrc = [&](int net) {
+          const WT *base = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n;
+          const uint64_t a = (uint64_t)base;
+          const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+          const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+          return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                                   (int)(H2 * C2 * (int)sizeof(WT)), 0x00020000);
+        };
+        auto issue = [&](int s, WT (&r)[K]) {
+          const int net = __builtin_amdgcn_readfirstlane(cf[3 + s / T]);
+          const int k0 = (s % T) * K;
+          const auto rsrc = net_rsrc(net);
+#pragma unroll
+          for (int it = 0; it < K; ++it) {
+            const int soff = (k0 + it * kRowsPerLoad * C2) * (int)sizeof(WT);
+            if constexpr (sizeof(WT) == 4) {
+              r[it] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lane_off, soff, 0));
+            } else {
+              const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, lane_off, soff, 0);
+              r[it] = __longlong_as_double((long long)(((uint64_t)v[1] << 32) | v[0]));
+            }
+          }
+        };
+        auto store = [&](const WT (&r)[K]) {
+#pragma unroll
+          for (int it = 0; it < K; ++it) {
+            const int f = it * kWideThreads + t;
+            tile[(f / K) * KP + (f % K)] = r[it];
+          }
+        };
+        auto compute = [&](int s) {
+          const int net = cf[3 + s / T], tl = s % T, k0 = tl * K;
+          const int kn = min(K, C2 - k0);
+          if (t >= H2) return;
+          const WT *tr = tile + t * KP;
+          if (net == 0) {
+            if (kn == K) {
+#pragma unroll 4
+              for (int k = 0; k < K; ++k) {
+                const double wk = (double)tr[k];
+                const double *hp = h1 + (k0 + k) * NC;
+#pragma unroll
+                for (int c = 0; c < NG; ++c) z[c] = __dadd_rn(z[c], __dmul_rn(wk, hp[c]));
+              }
+            } else {
+              for (int k = 0; k < kn; ++k) {
+                const double wk = (double)tr[k];
+                const double *hp = h1 + (k0 + k) * NC;
+#pragma unroll
+                for (int c = 0; c < NG; ++c) z[c] = __dadd_rn(z[c], __dmul_rn(wk, hp[c]));
+              }
+            }
+          } else {
+            const int col = NG + net - 1;
+            if (tl == 0) zo = 0.0;
+            const double *hp = h1 + k0 * NC + col;
+            if (kn == K) {
+#pragma unroll 8
+              for (int k = 0; k < K; ++k) zo = __dadd_rn(zo, __dmul_rn((double)tr[k], hp[k * NC]));
+            } else {
+              for (int k = 0; k < kn; ++k) zo = __dadd_rn(zo, __dmul_rn((double)tr[k], hp[k * NC]));
+            }
+            if (tl == T - 1) {
+#pragma unroll
+              for (int c = 0; c < NG; ++c)
+                if (c == net - 1) z[NG + c] = zo;
+            }
+          }
+        };
+
+        WT ra[K], rb[K];
+        issue(0, ra);
+        if (S > 1) issue(1, rb);
+        store(ra);
+        __syncthreads();
+        if (S > 2) issue(2, ra);
+        for (int s = 0; s < S; s += 2) {
+          compute(s);
+          __syncthreads();
+          if (s + 1 < S) {
+            store(rb);
+            __syncthreads();
+            if (s + 3 < S) issue(s + 3, rb);
+            compute(s + 1);
+            __syncthreads();
+            if (s + 2 < S) {
+              store(ra);
+              __syncthreads();
+              if (s + 4 < S) issue(s + 4, ra);
+            }
+          }
+        }
+        // every tile read is behind the last barrier: h2 may overwrite the tile
+        if (t < H2) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c) h2[t * NC + c] = ((mask >> c) & 1) ? sigmoid_f64(z[c]) : 0.0;
+        }
+        if (b && t < NC) h2[H2 * NC + t] = 1.0;
+        __syncthreads();
+
+        // ---- D: layer 3 + output sigmoid, one thread per (needed column, output)
+        const int nchain = __builtin_popcount(mask) * O;
+        if (t < nchain) {
+          const int o = t % O, c = nth_set_bit(mask, t / O);
+          const WT *v = (c < NG ? gbase : opponents + orow[c - NG]) + W1n + W2n + (long)o * C3;
+          const double *hp = h2 + c;
+          double zz = 0.0;
+          int j = 0;
+          for (; j + 8 <= C3; j += 8) {
+            double wv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) wv[u] = (double)v[j + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) zz = __dadd_rn(zz, __dmul_rn(wv[u], hp[(j + u) * NC]));
+          }
+          for (; j < C3; ++j) zz = __dadd_rn(zz, __dmul_rn((double)v[j], hp[j * NC]));
+          outv[c * 4 + o] = sigmoid_f64(zz);
+        }
+        __syncthreads();
+      }
+
+      // ---- E: actions, clamp, bookkeeping (main.py:88-107, 128-135)
+      if (wid == 0 && active) {
+        int right = 0;
+        if (vis) {
+          right = index_to_code(argmax_np(outv + lane * 4, O));
+          if (kind == kOppNN) left = index_to_code(argmax_np(outv + (NG + lane) * 4, O));
+          c_fwd += 1 + (kind == kOppNN ? 1 : 0);
+        }
+        act_l = clamp_action(lc2, left);
+        act_r = clamp_action(rc2, right);
+        if (p.trace && w < p.trace_games && frames <= p.trace_cap)
+          p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+        if (frames > 1) {
+          if (st.s1 == s1b && st.s2 == s2b) {
+            timeout += 1;
+          } else {
+            total += timeout;
+            timeout = 0;
+          }
+        }
+        if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
+          finish_game(p, w, st, frames, total);
+          active = false;
+          c_steps += frames;
+          c_games += 1;
+        }
+      }
+    }
+  }
+  if (p.counters && wid == 0 && c_games) {
+    atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)c_steps);
+    atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
+    atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
+  }
+  if (p.counters && t == 0 && c_streams)  // network passes: each streams W1, W2, W3 of one network once
+    atomicAdd((unsigned long long *)&p.counters[7], (unsigned long long)c_streams);
+}
+
+bool wide_shape_ok(const pg_net &n, int n_games) {
+  return n.n_nodes == 4 && n.nodes[0] == 6 && n.nodes[1] >= 1 && n.nodes[1] <= kWideThreads &&
+         n.nodes[2] >= 1 && n.nodes[2] <= kWideThreads && n.nodes[3] >= 1 && n.nodes[3] <= 4 &&
+         n_games >= 1 && n_games <= kWideMaxGames;
+}
+
+template <int NG, typename WT>
+static int32_t launch_wide_t(const EvalParams &p, hipStream_t s) {
+  const int lds = wide_lds_bytes(2 * NG, p.nodes[1], p.nodes[2], p.bias, (int)sizeof(WT), WideTile<WT>::KP);
+  if (lds > 160 * 1024) return fail(PG_ERR_UNSUPPORTED, "k_wide needs %d bytes of LDS", lds);
+  // above 64 KB of dynamic LDS; an older runtime that rejects the attribute launches anyway
+  (void)hipFuncSetAttribute((const void *)k_wide<NG, WT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  (void)hipGetLastError();
+  const int cap = num_cus();
+  const int grid = p.n_genomes < cap ? p.n_genomes : cap;
+  if (grid <= 0) return PG_OK;
+  hipLaunchKernelGGL((k_wide<NG, WT>), dim3(grid), dim3(kWideThreads), (size_t)lds, s, p);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t launch_wide(const EvalParams &p, int dtype, hipStream_t s) {
+  if (p.n_games <= 6)
+    return dtype == PG_F64 ? launch_wide_t<6, double>(p, s) : launch_wide_t<6, float>(p, s);
+  return dtype == PG_F64 ? launch_wide_t<8, double>(p, s) : launch_wide_t<8, float>(p, s);
+}
+
+}  // namespace pg

@@ -27,6 +27,7 @@
 
 #include "../../include/pong_ga.h"
 #include "pg_device.hpp"
+#include "pg_eval.hpp"
 #include "pg_f64math.h"
 
 #ifndef PG_VERSION_STRING
@@ -38,7 +39,7 @@ namespace pg {
 // --------------------------------------------------------------- errors ----
 static thread_local std::string g_last_error;
 
-static int32_t fail(int32_t code, const char *fmt, ...) {
+int32_t fail(int32_t code, const char *fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -48,62 +49,6 @@ static int32_t fail(int32_t code, const char *fmt, ...) {
   return code;
 }
 
-#define PG_HIP(call)                                                                  \
-  do {                                                                                \
-    hipError_t e_ = (call);                                                           \
-    if (e_ != hipSuccess)                                                             \
-      return fail(PG_ERR_HIP, "%s failed: %s", #call, hipGetErrorString(e_));        \
-  } while (0)
-
-// ------------------------------------------------------- kernel params ----
-struct EvalParams {
-  const void *genomes;
-  const void *opponents;
-  const int32_t *rows;  // unused (reserved)
-  const int32_t *kind;
-  const int32_t *opp;
-  const double *mult;
-  double *rewards;
-  int32_t *scores;
-  int32_t *frames;
-  double *total_frames;
-  int32_t *status_game;  // [n*games] scratch: zero-division per game
-  uint64_t *counters;
-  uint8_t *trace;
-  unsigned int *work;    // dynamic game counter (workspace)
-  int64_t gstride, ostride;
-  uint64_t seed;
-  int n_genomes, n_games, total;
-  int trace_games, trace_cap;
-  int nodes[PG_MAX_NODES];
-  int n_nodes, bias, max_width;
-};
-
-// Results of one finished game: perform_episode's return value and the
-// bookkeeping around it (main.py:108-112, utils.py:104-109).
-__device__ inline void finish_game(const EvalParams &p, int w, const Pong &st, int frames, int total) {
-  const double mult = p.mult[w];
-  double reward = 0.0;
-  int zero_div = 0;
-  if (st.s1 != st.s2) {
-    const double tf = (double)total;
-    if (tf == 0.0) {
-      zero_div = 1;
-      reward = __builtin_nan("");
-    } else {
-      // ((my - enemy) + my * mult) / (total_frames / 100.0), no contraction
-      const double diff = (double)(st.s2 - st.s1);
-      const double bonus = __dmul_rn((double)st.s2, mult);
-      reward = __dadd_rn(diff, bonus) / (tf / 100.0);
-    }
-  }
-  p.rewards[w] = reward;
-  p.scores[2 * w] = st.s1;
-  p.scores[2 * w + 1] = st.s2;
-  p.frames[w] = frames;
-  p.total_frames[w] = (double)total;
-  p.status_game[w] = zero_div;
-}
 
 // ===================================================== general (f64) path ==
 // One forward pass of NeuralNetwork.run (numpy_nn.py:120-137) by one wave, in
@@ -135,11 +80,6 @@ __device__ int forward_f64_wave(const WT *__restrict__ w, const int *nodes, int 
     if (__builtin_isnan(cur[j]) || cur[j] > cur[best]) best = j;
   return best;
 }
-
-// Features of utils.inference (utils.py:139-153) in f64 from doubled
-// centroids k: value = (k / 2) / 160, exactly the reference's rounding.
-__device__ inline double feat64(int k) { return __dmul_rn(0.5, (double)k) / 160.0; }
-__device__ inline double feat64_flip(int k) { return (160.0 - __dmul_rn(0.5, (double)k)) / 160.0; }
 
 template <typename WT>
 __global__ __launch_bounds__(64) void k_general(EvalParams p) {
@@ -1503,7 +1443,7 @@ static int max_width(const pg_net &n) {
 }
 
 static int g_num_cus = 0;
-static int num_cus() {
+int num_cus() {
   if (g_num_cus == 0) {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -1724,8 +1664,21 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   PG_HIP(hipMemsetAsync(a->workspace, 0, 256, s));
   int kernel = a->kernel;
   const bool res_ok = resident_shape_ok(a->net);
-  if (kernel == PG_KERNEL_AUTO) kernel = (res_ok && a->precision == PG_PREC_CERTIFIED) ? PG_KERNEL_SPLIT : PG_KERNEL_GENERAL;
-  if (kernel == PG_KERNEL_SPLIT) {
+  const bool wide_ok = wide_shape_ok(a->net, a->n_games);
+  if (kernel == PG_KERNEL_AUTO) {
+    if (res_ok && a->precision == PG_PREC_CERTIFIED)
+      kernel = PG_KERNEL_SPLIT;
+    else if (wide_ok && (a->net.nodes[1] >= 64 || a->net.nodes[2] >= 64))
+      kernel = PG_KERNEL_WIDE;
+    else
+      kernel = PG_KERNEL_GENERAL;
+  }
+  if (kernel == PG_KERNEL_WIDE) {
+    if (!wide_ok)
+      return fail(PG_ERR_UNSUPPORTED, "wide kernel needs NETWORK_SHAPE [6, H1<=512, H2<=512, 1..4] and n_games <= 8");
+    rc = launch_wide(p, a->net.dtype, s);
+    if (rc != PG_OK) return rc;
+  } else if (kernel == PG_KERNEL_SPLIT) {
     if (!res_ok) return fail(PG_ERR_UNSUPPORTED, "split kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
     if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "split kernel is the certified-precision path");
     const int H = a->net.nodes[1];

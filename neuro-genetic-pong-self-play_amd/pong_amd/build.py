@@ -8,9 +8,11 @@ import sys
 
 from ._lib import LIB_PATH, PKG_DIR, REPO_DIR
 
-SOURCES = [os.path.join(PKG_DIR, "csrc", "pong_ga.hip")]
-DEPS = SOURCES + [os.path.abspath(__file__), os.path.join(PKG_DIR, "csrc", "pg_device.hpp"), os.path.join(PKG_DIR, "csrc", "pg_f64math.h"),
-        os.path.join(REPO_DIR, "include", "pong_ga.h")]
+CSRC = os.path.join(PKG_DIR, "csrc")
+# one translation unit per kernel family, compiled in parallel and linked into one .so
+SOURCES = [os.path.join(CSRC, "pong_ga.hip"), os.path.join(CSRC, "pg_wide.hip")]
+DEPS = SOURCES + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp")] + [
+    os.path.join(REPO_DIR, "include", "pong_ga.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PG_OFFLOAD_ARCH", "gfx950")
 
@@ -25,15 +27,26 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB_PATH
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
-           # no SLP packing of independent f32 adds into v_pk_add_f32: it breaks the
-           # DPP-fused reductions into mov_dpp + pk_add pairs (measured -5 %)
-           "-fno-slp-vectorize", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO_DIR, "include"),
-           "-o", LIB_PATH + ".tmp"] + SOURCES
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
+             # no SLP packing of independent f32 adds into v_pk_add_f32: it breaks the
+             # DPP-fused reductions into mov_dpp + pk_add pairs (measured -5 %)
+             "-fno-slp-vectorize", "-fPIC",
+             "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO_DIR, "include")]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.splitext(os.path.basename(src))[0] + ".o")
+        cmd = [HIPCC] + flags + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((subprocess.Popen(cmd), cmd))
+        objs.append(obj)
+    for proc, cmd in procs:
+        if proc.wait() != 0:
+            raise subprocess.CalledProcessError(proc.returncode, cmd)
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", LIB_PATH + ".tmp"] + objs
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+        print(" ".join(link), file=sys.stderr)
+    subprocess.check_call(link)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
 

@@ -1,0 +1,134 @@
+"""k_wide (pg_wide.hip): wide two-hidden-layer networks, BASELINE config 5
+([6, 512, 512, 3]), against the C oracle and the one-wave-per-game general
+kernel (run with -m gpu).
+
+Bar: bit-exact scores, frames, total_frames, f64 rewards and fitness, and
+per-frame actions.  k_wide evaluates numpy_nn's own f64 operation sequence
+(numpy_nn.py:126-129) with k_general's sigmoid, so the two kernels agree
+bit for bit, not only on the decisions.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _gene_count(shape, bias=True):
+    b = 1 if bias else 0
+    return sum((shape[i] + b) * shape[i + 1] for i in range(len(shape) - 1))
+
+
+def _schedule(rng, n, n_games, n_opp, nn_frac=0.6):
+    kinds = rng.integers(0, 3, size=(n, n_games)).astype(np.int32)
+    kinds[rng.random((n, n_games)) < nn_frac] = 3
+    opp = rng.integers(0, n_opp, size=(n, n_games)).astype(np.int32)
+    mult = np.ones((n, n_games))
+    nn = kinds == 3
+    mult[nn] = np.round(rng.normal(size=nn.sum()), 3)
+    return kinds, opp, mult
+
+
+def _dev(a, gpu, dt):
+    return torch.tensor(np.ascontiguousarray(a), dtype=dt, device=gpu)
+
+
+def _eval(ev, gpu, genomes, opponents, kinds, opp, mult, **kw):
+    res, trace = ev.evaluate(_dev(genomes, gpu, ev.dtype), torch.tensor(kinds, device=gpu),
+                             torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
+                             opponents=_dev(opponents, gpu, ev.dtype), **kw)
+    torch.cuda.synchronize()
+    return res, trace
+
+
+def _same(a, b):
+    for name in ("scores", "frames", "total_frames", "rewards", "fitness", "status"):
+        y = b[name] if isinstance(b, dict) else getattr(b, name).cpu().numpy()
+        np.testing.assert_array_equal(getattr(a, name).cpu().numpy(), y, err_msg=name)
+
+
+@pytest.mark.parametrize("shape,bias,dt", [
+    ([6, 16, 8, 3], True, torch.float64),
+    ([6, 40, 24, 2], True, torch.float32),
+    ([6, 64, 64, 3], False, torch.float64),
+    ([6, 100, 130, 4], True, torch.float32),
+])
+def test_wide_matches_oracle(gpu, oracle, shape, bias, dt):
+    from pong_amd.device import Evaluator
+    rng = np.random.default_rng(sum(shape))
+    G = _gene_count(shape, bias)
+    n, H = 21, 5
+    genomes = (rng.standard_normal((n, G)) * 2.0)
+    opponents = (rng.standard_normal((H, G)) * 2.0)
+    if dt == torch.float32:
+        genomes = genomes.astype(np.float32).astype(np.float64)
+        opponents = opponents.astype(np.float32).astype(np.float64)
+    kinds, opp, mult = _schedule(rng, n, 6, H)
+    ev = Evaluator(shape, bias=bias, dtype=dt, device=gpu, kernel="wide")
+    res, _ = _eval(ev, gpu, genomes, opponents, kinds, opp, mult)
+    ref = oracle.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents, bias=bias, n_threads=8)
+    _same(res, ref)
+    assert int(res.counters[0]) == int(ref["frames"].sum())
+    assert int(res.counters[3]) == n * 6
+
+
+@pytest.mark.parametrize("n_games", [1, 3, 6, 7, 8])
+def test_wide_equals_general_with_traces(gpu, n_games):
+    """Every column count (NG = 6 and 8 instantiations, partial columns), both
+    paddles' per-frame actions, against the one-wave-per-game f64 kernel."""
+    from pong_amd.device import Evaluator
+    shape = [6, 96, 80, 3]
+    rng = np.random.default_rng(100 + n_games)
+    G = _gene_count(shape)
+    n, H = 13, 4
+    genomes, opponents = rng.standard_normal((n, G)) * 3.0, rng.standard_normal((H, G)) * 3.0
+    kinds, opp, mult = _schedule(rng, n, n_games, H, nn_frac=0.8)
+    ev = Evaluator(shape, device=gpu, n_games=n_games)
+    cap = 3000
+    rw, tw = _eval(ev, gpu, genomes, opponents, kinds, opp, mult, kernel="wide", trace_games=n * n_games, trace_cap=cap)
+    rg, tg = _eval(ev, gpu, genomes, opponents, kinds, opp, mult, kernel="general", trace_games=n * n_games,
+                   trace_cap=cap)
+    _same(rw, rg)
+    assert torch.equal(tw, tg)
+    assert torch.equal(rw.counters[:4], rg.counters[:4])
+
+
+def test_wide_config5_shape_matches_oracle(gpu, oracle):
+    """[6, 512, 512, 3] (config 5), f32 genome storage, self-play and scripted
+    games: whole evaluations equal the oracle's."""
+    from pong_amd.device import Evaluator
+    shape = [6, 512, 512, 3]
+    rng = np.random.default_rng(512)
+    G = _gene_count(shape)
+    n, H = 3, 2
+    genomes = (rng.standard_normal((n, G)) * 3.0).astype(np.float32).astype(np.float64)
+    opponents = (rng.standard_normal((H, G)) * 3.0).astype(np.float32).astype(np.float64)
+    kinds = np.array([[0, 1, 2, 3, 3, 3], [3, 3, 3, 3, 3, 3], [3, 0, 3, 1, 3, 2]], np.int32)
+    opp = rng.integers(0, H, size=(n, 6)).astype(np.int32)
+    mult = np.ones((n, 6))
+    ev = Evaluator(shape, dtype=torch.float32, device=gpu)  # AUTO picks the wide kernel
+    res, _ = _eval(ev, gpu, genomes, opponents, kinds, opp, mult)
+    ref = oracle.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents, n_threads=8)
+    _same(res, ref)
+
+
+def test_wide_selfplay_properties(gpu):
+    """A few hundred genomes of the config-5 shape: deterministic, and
+    permutation-equivariant (a genome's result does not depend on which
+    workgroup or slot evaluated it)."""
+    from pong_amd.device import Evaluator
+    shape = [6, 512, 512, 3]
+    G = _gene_count(shape)
+    n, H = 320, 80
+    gen = torch.Generator(device=gpu).manual_seed(7)
+    genomes = torch.randn((n, G), generator=gen, dtype=torch.float32, device=gpu) * 3.0
+    opponents = genomes[:H].contiguous()
+    ev = Evaluator(shape, dtype=torch.float32, device=gpu)
+    kind, opp, mult = ev.selfplay_schedule(n, H)
+    r1, _ = ev.evaluate(genomes, kind, opp, mult, opponents=opponents)
+    f1 = r1.fitness.clone()
+    perm = torch.randperm(n, device=gpu)
+    r2, _ = ev.evaluate(genomes[perm].contiguous(), kind[perm].contiguous(), opp[perm].contiguous(),
+                        mult[perm].contiguous(), opponents=opponents)
+    assert torch.equal(r2.fitness, f1[perm]) and torch.equal(r2.frames, r1.frames[perm])
+    assert int(r1.counters[3]) == n * 6 and int(r1.counters[0]) == int(r1.frames.sum())
