@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Headline benchmark: the GA evaluation loop at population 65 536 per GPU.
 
+--config wide runs BASELINE config 5 instead: the same generation step for the
+wide MLP [6,512,512,3] (f32 genome storage, k_wide streaming kernel).
+
 One step = one GA generation of the reference's eaSimple loop
 (main.py:165-170) on device:
   1. evaluate every genome's 6 self-play games to termination
@@ -37,13 +40,15 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
 
 def parse():
     p = argparse.ArgumentParser()
+    p.add_argument("--config", default="selfplay", choices=["selfplay", "wide"],
+                   help="selfplay = BASELINE config 3 ([6,64,3], the headline); wide = config 5 ([6,512,512,3])")
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=None)
+    p.add_argument("--warmup", type=int, default=None)
     p.add_argument("--pop", type=int, default=65536, help="genomes evaluated per GPU")
-    p.add_argument("--shape", default="6,64,3")
+    p.add_argument("--shape", default=None)
     p.add_argument("--games", type=int, default=6)
-    p.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    p.add_argument("--dtype", default=None, choices=["float64", "float32"])
     p.add_argument("--group-lanes", type=int, default=0)
     p.add_argument("--kernel", default="auto")
     p.add_argument("--sigma", type=float, default=3.0)
@@ -51,7 +56,14 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    return p.parse_args()
+    a = p.parse_args()
+    wide = a.config == "wide"
+    # presets: a wide generation takes ~30 s at 65 536 genomes, so fewer steps
+    a.steps = a.steps if a.steps is not None else (1 if wide else 5)
+    a.warmup = a.warmup if a.warmup is not None else (0 if wide else 1)
+    a.shape = a.shape or ("6,512,512,3" if wide else "6,64,3")
+    a.dtype = a.dtype or ("float32" if wide else "float64")
+    return a
 
 
 def main():
@@ -86,7 +98,11 @@ def main():
     # population, so the HoF candidates (HoF + population) are one gather.
     gen = torch.Generator(device=dev).manual_seed(args.seed)
     store = torch.empty((H + P, G), dtype=dtype, device=dev)
-    store[H:] = torch.randn((P, G), generator=gen, dtype=torch.float64, device=dev).mul_(args.sigma).to(dtype)
+    rows = max(1, (1 << 30) // (8 * G))  # draw in ~1 GB chunks (the wide population is 70 GB in f32)
+    for r0 in range(0, P, rows):
+        r1 = min(P, r0 + rows)
+        store[H + r0:H + r1] = torch.randn((r1 - r0, G), generator=gen, dtype=torch.float64,
+                                           device=dev).mul_(args.sigma).to(dtype)
     store[:H] = store[H:H + H]
     spare = torch.empty_like(store)
     hof_fit = torch.full((H,), -1e300, dtype=torch.float64, device=dev)
@@ -131,6 +147,7 @@ def main():
     fwd_local = 0
     slow_local = 0
     cert_local = [0, 0, 0]  # certificate failures, decided by the service wave, decided in-wave
+    passes_local = 0        # k_wide: network weight passes (each streams one network's genes once)
     kernel_ms = []
     counters = []
     for s in range(args.steps):
@@ -152,9 +169,10 @@ def main():
         slow_local += int(c[2])
         for i in range(3):
             cert_local[i] += int(c[4 + i])
+        passes_local += int(c[7])
 
     t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)]
-                     + [float(v) for v in cert_local], dtype=torch.float64, device=dev)
+                     + [float(v) for v in cert_local] + [float(passes_local)], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
@@ -164,12 +182,21 @@ def main():
         steps_all, fwd_all, slow_all = float(tsum[1]), float(tsum[2]), float(tsum[3])
         kernel_ms_mean = float(tsum[4]) / world / args.steps
         cert_all = [float(v) for v in tsum[5:8]]
+        passes_all = float(tsum[8])
     else:
         steps_all, fwd_all, slow_all = float(t[1]), float(t[2]), float(t[3])
         kernel_ms_mean = float(t[4]) / args.steps
         cert_all = [float(v) for v in t[5:8]]
+        passes_all = float(t[8])
 
-    if rank == 0:
+    if rank == 0 and args.config == "wide":
+        out = wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all,
+                          passes_all, kernel_ms_mean)
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, shape, store[H:], store[:H], kind, opp, mult, lo, chunk=8,
+                                              max_rows=256)
+        print(json.dumps(out), flush=True)
+    elif rank == 0:
         env_steps_per_s = steps_all / elapsed
         ms_per_step = elapsed * 1000.0 / args.steps
         # roofline of the dominant kernel (k_resident), per launch on rank 0's timing
@@ -226,16 +253,68 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo):
+def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all, passes_all,
+                kernel_ms_mean):
+    """BASELINE config 5: the generation step with the wide MLP; k_wide is
+    HBM-bound (its W2 stream), so the roofline is bytes of weights streamed
+    per launch over the launch time against the 8 TB/s HBM peak."""
+    wt = 4 if dtype == torch.float32 else 8
+    ms_per_step = elapsed * 1000.0 / args.steps
+    passes_per_launch = passes_all / world / args.steps
+    steps_per_launch = steps_all / world / args.steps
+    bytes_per_launch = passes_per_launch * G * wt
+    achieved = bytes_per_launch / (kernel_ms_mean / 1e3) / 1e9
+    survey_bytes = steps_per_launch * (2 * 4 * G + 128)  # SURVEY 8d: both networks streamed per env-step
+    return {
+        "metric": "env-steps/sec (GA evaluation loop, self-play, wide MLP) + generations/sec at pop=65536 per GPU",
+        "value": steps_all / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "generations_per_sec": 1000.0 / ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64 (numpy_nn's operation order); genomes " + ("f32" if wt == 4 else "f64"),
+        "data": "synthetic N(0,%g) genomes, random-init [%s] MLPs, self-play vs hall of fame" % (args.sigma, args.shape),
+        "config": {"workload": "BASELINE config 5: population 65536 per GPU, wide MLP [6,512,512,3], 6 self-play "
+                               "games per genome, device GA step (selTournament/varAnd/HoF)",
+                   "population": P, "population_per_gpu": n_local, "network_shape": shape,
+                   "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
+                   "parallelism": f"dp{world}" if world > 1 else "dp1",
+                   "env_steps_per_generation": steps_all / args.steps,
+                   "network_passes_per_generation": passes_all / args.steps,
+                   "forwards_per_network_pass": fwd_all / max(passes_all, 1.0)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic("pmc_traffic_wide.json"),
+                     "kernel": "k_wide<6,float> (pg_eval_population: one 512-thread workgroup per genome, six games "
+                               "in lockstep, W2 streamed HBM->registers->LDS once per frame per network)",
+                     "kernel_ms_per_launch": kernel_ms_mean,
+                     "bytes_per_network_pass": G * wt,
+                     "network_passes_per_launch": passes_per_launch,
+                     "survey_algorithmic_GBps": survey_bytes / (kernel_ms_mean / 1e3) / 1e9,
+                     "note": "achieved = genome bytes streamed (network passes x genes x 4 B) / launch time; "
+                             "survey_algorithmic counts both networks' genes per env-step (SURVEY 8d), which the "
+                             "lockstep genome pass amortises over the genome's games"},
+    }
+
+
+def cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo, chunk=256, max_rows=1 << 16):
     """The CPU oracle (C restatement of the reference loop, f64 numpy_nn
     arithmetic) on the same workload's first genomes, on the host cores."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     O.build()
-    genomes = pop[lo:lo + (1 << 16)].double().cpu().numpy()
-    opponents = hof.double().cpu().numpy()
-    k, o, m = kind.cpu().numpy(), opp.cpu().numpy(), mult.cpu().numpy()
-    steps, done, chunk = 0, 0, 256
+    genomes = pop[lo:lo + max_rows].double().cpu().numpy()
+    n = genomes.shape[0]
+    k, o, m = kind[:n].cpu().numpy(), opp[:n].cpu().numpy(), mult[:n].cpu().numpy()
+    # only the hall-of-fame rows these genomes play (the wide HoF is 35 GB in f64)
+    rows = np.unique(o)
+    opponents = hof[torch.as_tensor(rows, device=hof.device)].double().cpu().numpy()
+    o = np.searchsorted(rows, o).astype(np.int32)
+    steps, done = 0, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < args.cpu_baseline_seconds and done + chunk <= genomes.shape[0]:
         r = O.eval_population(genomes[done:done + chunk], shape, k[done:done + chunk], o[done:done + chunk],
@@ -249,9 +328,9 @@ def cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo):
             "cpu": _cpu_model()}
 
 
-def _pmc_traffic():
+def _pmc_traffic(name="pmc_traffic.json"):
     try:
-        with open(os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")) as fh:
+        with open(os.path.join(REPO, "profiles", "r01", name)) as fh:
             return json.load(fh)["traffic_bytes"]
     except (OSError, ValueError, KeyError):
         return None

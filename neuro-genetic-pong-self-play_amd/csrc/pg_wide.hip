@@ -30,28 +30,29 @@ namespace pg {
 constexpr int kWideThreads = 512;  // = max H2: one W2 row per thread
 constexpr int kWideMaxGames = 8;
 
-template <typename WT>
-struct WideTile;
-template <>
-struct WideTile<float> {
-  static constexpr int K = 32, KP = 33;  // 128 B of a row per tile; odd pitch: conflict-free row reads
-};
-template <>
-struct WideTile<double> {
-  static constexpr int K = 16, KP = 17;
-};
+// W2 tile: 128 B of each of the 512 rows, at a 144 B pitch in LDS (16 lanes'
+// ds_read_b128 of their own rows hit 16 distinct 16-B bank groups).
+constexpr int kTileRowBytes = 128, kTilePitch = 144;
+#ifndef PG_WIDE_DEPTH
+#define PG_WIDE_DEPTH 2
+#endif
+constexpr int kDepth = PG_WIDE_DEPTH;  // register sets in the W2 tile ring (2 and 3 measured equal)
 
 // LDS carve (bytes): feats [NC][8] f64 | outputs [NC][4] f64 | control |
-// h1 [C2][NC] f64 | tile [512][KP] WT, reused for h2 [C3][NC] f64 after layer 2.
+// h1 [C2][NC] f64 | tile [512][144 B], reused for h2 [C3][NC] f64 after layer 2.
 constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffH1 = 2048;
 __host__ __device__ constexpr int align16(int v) { return (v + 15) & ~15; }
 
-__host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b, int wt_bytes, int KP) {
+__host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b) {
   const int h1 = align16((H1 + b) * NC * 8);
-  const int tile = kWideThreads * KP * wt_bytes;
+  const int tile = kWideThreads * kTilePitch;
   const int h2 = align16((H2 + b) * NC * 8);
   return kOffH1 + h1 + (tile > h2 ? tile : h2);
 }
+
+// numpy's sigmoid, out of line: one copy of the libm pow instead of one per
+// unrolled column keeps the layer loops' register pressure low
+__device__ __noinline__ double sigmoid_f64_call(double z) { return sigmoid_f64(z); }
 
 // index of the q-th set bit of m (q < popcount(m))
 __device__ __forceinline__ int nth_set_bit(unsigned m, int q) {
@@ -67,11 +68,31 @@ __device__ __forceinline__ int argmax_np(const double *v, int O) {
   return best;
 }
 
+// Diagnostic build (-DPG_WIDE_STAMPS): thread 0 adds the shader-clock cycles
+// between the frame's phase boundaries into counters[4..6] (A+E+B, C, D).
+#ifdef PG_WIDE_STAMPS
+#define PG_STAMP(i)                                                        \
+  do {                                                                     \
+    if (t == 0) {                                                          \
+      const uint64_t now_ = __builtin_amdgcn_s_memtime();                  \
+      stamp_acc[(i) == 0 ? 0 : (i) == 1 ? 0 : (i) == 2 ? 1 : 2] += now_ - stamp_last; \
+      stamp_last = now_;                                                   \
+    }                                                                      \
+  } while (0)
+#else
+#define PG_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 template <int NG, typename WT>
 __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
+#ifdef PG_WIDE_STAMPS
+  uint64_t stamp_acc[3] = {0, 0, 0}, stamp_last = __builtin_amdgcn_s_memtime();
+#endif
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int NC = 2 * NG;  // columns: right (genome) of game c = c, left (opponent) of game c = NG + c
-  constexpr int K = WideTile<WT>::K, KP = WideTile<WT>::KP;
+  constexpr int K = kTileRowBytes / (int)sizeof(WT);
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int b = p.bias;
   const int H1 = p.nodes[1], H2 = p.nodes[2], O = p.nodes[3];
@@ -84,7 +105,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   int *ctl = (int *)(lds_raw + kOffCtl);         // [0] genome; frame-parity halves at [8..] and [40..]
   long long *orow = (long long *)(lds_raw + kOffOrow);  // [NG] opponent row offsets (elements)
   double *h1 = (double *)(lds_raw + kOffH1);            // [C2][NC]
-  WT *tile = (WT *)(lds_raw + kOffH1 + align16(C2 * NC * 8));
+  unsigned char *tile = lds_raw + kOffH1 + align16(C2 * NC * 8);
   double *h2 = (double *)tile;  // [C3][NC], after layer 2
 
   const WT *genomes = (const WT *)p.genomes;
@@ -155,6 +176,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
         }
       }
       __syncthreads();
+      PG_STAMP(0);
       const unsigned mask = (unsigned)cf[0];
       if (!cf[1]) break;
       const int n_nets = cf[2];
@@ -174,7 +196,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
               const double *x = feat + c * 8;
               double z = 0.0;
               for (int i = 0; i < C1; ++i) z = __dadd_rn(z, __dmul_rn(wv[i], x[i]));
-              h1[j * NC + c] = sigmoid_f64(z);
+              h1[j * NC + c] = sigmoid_f64_call(z);
             }
           }
 #pragma unroll
@@ -184,143 +206,179 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             const double *x = feat + (NG + c) * 8;
             double z = 0.0;
             for (int i = 0; i < C1; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], x[i]));
-            h1[j * NC + NG + c] = sigmoid_f64(z);
+            h1[j * NC + NG + c] = sigmoid_f64_call(z);
           }
         }
         if (b && t < NC) h1[H1 * NC + t] = 1.0;
         __syncthreads();
+        PG_STAMP(1);
 
-        // ---- C: layer 2, W2 streamed in tiles; thread t accumulates row t
-        double z[NC];
+        // ---- C: layer 2, W2 streamed in tiles; thread t accumulates row t.
+        // A tile is 128 B of every row (K = 128 / sizeof(WT) columns); lane
+        // t loads 16 B pieces (chunk t % 8 of rows t / 8 + 64 it), so each
+        // wave-instruction reads 8 rows x 128 B.  Tiles pass through a ring
+        // of kDepth register sets: while tile s is multiplied out of LDS,
+        // tiles s+1 .. s+kDepth are in flight.
+        double zg[NG];   // the genome's row sums (one per game)
+        double zop[NG];  // finished opponents' row sums (written once per network pass)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) z[c] = 0.0;
+        for (int c = 0; c < NG; ++c) { zg[c] = 0.0; zop[c] = 0.0; }
         double zo = 0.0;  // the current opponent network's row sum
         const int S = n_nets * T;
-        // W2 rows through a buffer descriptor per network: the per-lane part of
-        // the offset is fixed (row t / K, column t % K of a tile), the rest is
-        // a scalar, so a tile's K loads cost no address registers; rows past
-        // H2 fall outside num_records and read 0.
-        const int lane_off = ((t / K) * C2 + (t % K)) * (int)sizeof(WT);
-        constexpr int kRowsPerLoad = kWideThreads / K;
-        auto net_rsrc = [&](int net) {
+        const int lane_off = (t >> 3) * C2 * (int)sizeof(WT) + (t & 7) * 16;
+        const int w2_bytes = H2 * C2 * (int)sizeof(WT);
+        // Steps s >= S load through an empty descriptor (no memory traffic), so
+        // every issue is unconditional and the waits stay counted.
+        // Tile s+kDepth's loads are spread over tile s's arithmetic (one
+        // 16-B piece per piece of work): a wave whose loads cannot all be
+        // accepted at once keeps computing instead of stalling at the issue.
+        struct Src {
+          __amdgpu_buffer_rsrc_t rsrc;
+          int k0;
+        };
+        auto source = [&](int s) -> Src {
+          const bool valid = s < S;
+          const int net = valid ? __builtin_amdgcn_readfirstlane(cf[3 + s / T]) : 0;
+          const int k0 = valid ? (s % T) * K : 0;
           const WT *base = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n;
-          const uint64_t a = (uint64_t)base;
-          const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-          const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-          return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
-                                                   (int)(H2 * C2 * (int)sizeof(WT)), 0x00020000);
+          const uint64_t ad = (uint64_t)base;
+          const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ad);
+          const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32));
+          return {__builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                                    valid ? w2_bytes : 0, 0x00020000),
+                  k0};
         };
-        auto issue = [&](int s, WT (&r)[K]) {
-          const int net = __builtin_amdgcn_readfirstlane(cf[3 + s / T]);
-          const int k0 = (s % T) * K;
-          const auto rsrc = net_rsrc(net);
+        auto load = [&](const Src &src, int it) -> uint4 {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+              src.rsrc, lane_off, (src.k0 + it * 64 * C2) * (int)sizeof(WT), 0);
+          return make_uint4(v[0], v[1], v[2], v[3]);
+        };
+        auto store = [&](const uint4 (&r)[8]) {
 #pragma unroll
-          for (int it = 0; it < K; ++it) {
-            const int soff = (k0 + it * kRowsPerLoad * C2) * (int)sizeof(WT);
-            if constexpr (sizeof(WT) == 4) {
-              r[it] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lane_off, soff, 0));
-            } else {
-              const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, lane_off, soff, 0);
-              r[it] = __longlong_as_double((long long)(((uint64_t)v[1] << 32) | v[0]));
-            }
-          }
+          for (int it = 0; it < 8; ++it)
+            *(uint4 *)((unsigned char *)tile + (it * 64 + (t >> 3)) * kTilePitch + (t & 7) * 16) = r[it];
         };
-        auto store = [&](const WT (&r)[K]) {
+        // multiply tile s (in LDS) into the row sums and load tile sn into r
+        auto compute = [&](int s, uint4 (&r)[8], int sn) {
+          const Src src = source(sn);
+          bool work = s < S && t < H2;
+#ifdef PG_WIDE_NOCOMPUTE
+          work = false;  // diagnostic build: streaming only
+#endif
+          if (!work) {
 #pragma unroll
-          for (int it = 0; it < K; ++it) {
-            const int f = it * kWideThreads + t;
-            tile[(f / K) * KP + (f % K)] = r[it];
+            for (int q = 0; q < 8; ++q) r[q] = load(src, q);
+            return;
           }
-        };
-        auto compute = [&](int s) {
           const int net = cf[3 + s / T], tl = s % T, k0 = tl * K;
           const int kn = min(K, C2 - k0);
-          if (t >= H2) return;
-          const WT *tr = tile + t * KP;
+          const unsigned char *tr = (const unsigned char *)tile + t * kTilePitch;
+          constexpr int E = 16 / (int)sizeof(WT);  // weights per 16-B piece
           if (net == 0) {
-            if (kn == K) {
-#pragma unroll 4
-              for (int k = 0; k < K; ++k) {
-                const double wk = (double)tr[k];
-                const double *hp = h1 + (k0 + k) * NC;
 #pragma unroll
-                for (int c = 0; c < NG; ++c) z[c] = __dadd_rn(z[c], __dmul_rn(wk, hp[c]));
-              }
-            } else {
-              for (int k = 0; k < kn; ++k) {
-                const double wk = (double)tr[k];
-                const double *hp = h1 + (k0 + k) * NC;
+            for (int q = 0; q < 8; ++q) {
+              const uint4 v = *(const uint4 *)(tr + q * 16);
+              r[q] = load(src, q);
+              WT wq[E];
+              __builtin_memcpy(wq, &v, 16);
 #pragma unroll
-                for (int c = 0; c < NG; ++c) z[c] = __dadd_rn(z[c], __dmul_rn(wk, hp[c]));
+              for (int e = 0; e < E; ++e) {
+                const int k = q * E + e;
+                if (k < kn) {
+                  const double wk = (double)wq[e];
+                  const double *hp = h1 + (k0 + k) * NC;
+#pragma unroll
+                  for (int c = 0; c < NG; ++c) zg[c] = __dadd_rn(zg[c], __dmul_rn(wk, hp[c]));
+                }
               }
             }
           } else {
-            const int col = NG + net - 1;
-            if (tl == 0) zo = 0.0;
-            const double *hp = h1 + k0 * NC + col;
-            if (kn == K) {
-#pragma unroll 8
-              for (int k = 0; k < K; ++k) zo = __dadd_rn(zo, __dmul_rn((double)tr[k], hp[k * NC]));
-            } else {
-              for (int k = 0; k < kn; ++k) zo = __dadd_rn(zo, __dmul_rn((double)tr[k], hp[k * NC]));
-            }
-            if (tl == T - 1) {
+            const double *hp = h1 + k0 * NC + NG + net - 1;
+            double acc = tl == 0 ? 0.0 : zo;
 #pragma unroll
-              for (int c = 0; c < NG; ++c)
-                if (c == net - 1) z[NG + c] = zo;
+            for (int q = 0; q < 8; ++q) {
+              const uint4 v = *(const uint4 *)(tr + q * 16);
+              r[q] = load(src, q);
+              WT wq[E];
+              __builtin_memcpy(wq, &v, 16);
+#pragma unroll
+              for (int e = 0; e < E; ++e) {
+                const int k = q * E + e;
+                if (k < kn) acc = __dadd_rn(acc, __dmul_rn((double)wq[e], hp[k * NC]));
+              }
             }
+            zo = acc;
+            if (tl == T - 1) zop[net - 1] = acc;  // once per network pass
           }
         };
 
-        WT ra[K], rb[K];
-        issue(0, ra);
-        if (S > 1) issue(1, rb);
-        store(ra);
+        // ring: before step s, LDS holds tile s, set s % kDepth is free and
+        // sets (s+1 .. s+kDepth-1) % kDepth hold tiles in flight
+        uint4 R[kDepth][8];
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d) {
+          const Src src = source(d);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) R[d][q] = load(src, q);
+        }
+        store(R[0]);
         __syncthreads();
-        if (S > 2) issue(2, ra);
-        for (int s = 0; s < S; s += 2) {
-          compute(s);
-          __syncthreads();
-          if (s + 1 < S) {
-            store(rb);
+        for (int s = 0; s < S; s += kDepth) {
+#pragma unroll
+          for (int d = 0; d < kDepth; ++d) {
+            compute(s + d, R[d], s + d + kDepth);
             __syncthreads();
-            if (s + 3 < S) issue(s + 3, rb);
-            compute(s + 1);
+            store(R[(d + 1) % kDepth]);  // tile s+d+1
             __syncthreads();
-            if (s + 2 < S) {
-              store(ra);
-              __syncthreads();
-              if (s + 4 < S) issue(s + 4, ra);
-            }
           }
         }
         // every tile read is behind the last barrier: h2 may overwrite the tile
         if (t < H2) {
 #pragma unroll
-          for (int c = 0; c < NC; ++c) h2[t * NC + c] = ((mask >> c) & 1) ? sigmoid_f64(z[c]) : 0.0;
+          for (int c = 0; c < NC; ++c) {
+            const double zc = c < NG ? zg[c] : zop[c - NG];
+            h2[t * NC + c] = ((mask >> c) & 1) ? sigmoid_f64_call(zc) : 0.0;
+          }
         }
         if (b && t < NC) h2[H2 * NC + t] = 1.0;
         __syncthreads();
+        PG_STAMP(2);
 
-        // ---- D: layer 3 + output sigmoid, one thread per (needed column, output)
-        const int nchain = __builtin_popcount(mask) * O;
-        if (t < nchain) {
-          const int o = t % O, c = nth_set_bit(mask, t / O);
-          const WT *v = (c < NG ? gbase : opponents + orow[c - NG]) + W1n + W2n + (long)o * C3;
-          const double *hp = h2 + c;
-          double zz = 0.0;
-          int j = 0;
-          for (; j + 8 <= C3; j += 8) {
-            double wv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) wv[u] = (double)v[j + u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) zz = __dadd_rn(zz, __dmul_rn(wv[u], hp[(j + u) * NC]));
+        // ---- D: layer 3 + output sigmoid, one thread per (needed column, output).
+        // The needed networks' W3 rows are first staged into the h1 region
+        // (dead after layer 2) by all threads with coalesced loads, as many
+        // networks at a time as fit, so the sequential sums read only LDS.
+        {
+          WT *w3s = (WT *)h1;
+          const int per_net = O * C3;
+          const int cap = (C2 * NC * 8) / (per_net * (int)sizeof(WT));
+          const unsigned rbits = mask & ((1u << NG) - 1);
+          for (int g0 = 0; g0 < n_nets; g0 += cap) {
+            const int gn = min(cap, n_nets - g0);
+            for (int i = t; i < gn * per_net; i += kWideThreads) {
+              const int slot = i / per_net, net = cf[3 + g0 + slot];
+              const WT *v = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n + W2n;
+              w3s[i] = v[i - slot * per_net];
+            }
+            __syncthreads();
+            const int nchain = __builtin_popcount(mask) * O;
+            if (t < nchain) {
+              const int o = t % O, c = nth_set_bit(mask, t / O);
+              // position of this column's network in the frame's network list
+              const int pos = c < NG ? 0 : (rbits ? 1 : 0) + __builtin_popcount((mask >> NG) & ((1u << (c - NG)) - 1));
+              if (pos >= g0 && pos < g0 + gn) {
+                const WT *v = w3s + (pos - g0) * per_net + o * C3;
+                const double *hp = h2 + c;
+                double zz = 0.0;
+#pragma unroll 8
+                for (int j = 0; j < C3; ++j) zz = __dadd_rn(zz, __dmul_rn((double)v[j], hp[j * NC]));
+                outv[c * 4 + o] = sigmoid_f64_call(zz);
+              }
+            }
+            __syncthreads();
           }
-          for (; j < C3; ++j) zz = __dadd_rn(zz, __dmul_rn((double)v[j], hp[j * NC]));
-          outv[c * 4 + o] = sigmoid_f64(zz);
         }
-        __syncthreads();
+        PG_STAMP(3);
       }
 
       // ---- E: actions, clamp, bookkeeping (main.py:88-107, 128-135)
@@ -357,6 +415,10 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
     atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
     atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
   }
+#ifdef PG_WIDE_STAMPS
+  if (p.counters && t == 0)
+    for (int i = 0; i < 3; ++i) atomicAdd((unsigned long long *)&p.counters[4 + i], (unsigned long long)stamp_acc[i]);
+#endif
   if (p.counters && t == 0 && c_streams)  // network passes: each streams W1, W2, W3 of one network once
     atomicAdd((unsigned long long *)&p.counters[7], (unsigned long long)c_streams);
 }
@@ -369,7 +431,7 @@ bool wide_shape_ok(const pg_net &n, int n_games) {
 
 template <int NG, typename WT>
 static int32_t launch_wide_t(const EvalParams &p, hipStream_t s) {
-  const int lds = wide_lds_bytes(2 * NG, p.nodes[1], p.nodes[2], p.bias, (int)sizeof(WT), WideTile<WT>::KP);
+  const int lds = wide_lds_bytes(2 * NG, p.nodes[1], p.nodes[2], p.bias);
   if (lds > 160 * 1024) return fail(PG_ERR_UNSUPPORTED, "k_wide needs %d bytes of LDS", lds);
   // above 64 KB of dynamic LDS; an older runtime that rejects the attribute launches anyway
   (void)hipFuncSetAttribute((const void *)k_wide<NG, WT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

@@ -8,25 +8,26 @@ WRITE_SIZE are in KiB per dispatch and count the L2's memory-side requests
 bytes of 16-B-per-lane streaming loads -- the genome loads here are 8-B
 scattered per-lane loads, a width the guide leaves uncalibrated, so the raw
 value is reported beside the x2 upper reading.
-usage: python tools/pmc_traffic.py gpurun_out/r16 profiles/r01/pmc_traffic.json
+usage: python tools/pmc_traffic.py gpurun_out/r16 profiles/r01/pmc_traffic.json [kernel-name-substring]
 """
 import csv
 import json
 import sys
 
 
-def mean_counter(path, name):
+def mean_counter(path, name, kernel="k_service"):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if "k_service" in r["Kernel_Name"] and r["Counter_Name"] == name]
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
     return sum(vals) / len(vals), len(vals)
 
 
 def main():
     run, out = sys.argv[1], sys.argv[2]
-    fetch, nf = mean_counter(f"{run}/pmc_FETCH_SIZE/pmc_counter_collection.csv", "FETCH_SIZE")
-    write, nw = mean_counter(f"{run}/pmc_WRITE_SIZE/pmc_counter_collection.csv", "WRITE_SIZE")
+    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_service"
+    fetch, nf = mean_counter(f"{run}/pmc_FETCH_SIZE/pmc_counter_collection.csv", "FETCH_SIZE", kernel)
+    write, nw = mean_counter(f"{run}/pmc_WRITE_SIZE/pmc_counter_collection.csv", "WRITE_SIZE", kernel)
     kib = 1024.0
-    res = {"kernel": "k_service", "dispatches": [nf, nw],
+    res = {"kernel": kernel, "dispatches": [nf, nw],
            "fetch_bytes_raw": fetch * kib, "write_bytes": write * kib,
            "traffic_bytes": (fetch + write) * kib,
            "traffic_bytes_fetch_x2": (2 * fetch + write) * kib,

@@ -16,7 +16,7 @@ from pong_amd import device as D  # noqa: E402
 pop = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 hof = int(sys.argv[2]) if len(sys.argv) > 2 else max(pop // 4, 1)
 dtype = torch.float32 if (len(sys.argv) <= 3 or sys.argv[3] == "f32") else torch.float64
-shape = [6, 512, 512, 3]
+shape = [int(v) for v in os.environ.get("PG_SHAPE", "6,512,512,3").split(",")]
 dev = torch.device("cuda", 0)
 ev = D.Evaluator(shape, dtype=dtype, device=dev, kernel=os.environ.get("PG_KERNEL", "wide"))
 gen = torch.Generator(device=dev).manual_seed(1234)
@@ -39,3 +39,6 @@ for rep in range(2):
           f"({c[0] / (ms / 1e3):.3e}/s), forwards {c[1]}, games {c[3]}, network passes {c[7]}, "
           f"weight bytes {wb:.3e} = {wb / (ms / 1e3) / 1e9:.0f} GB/s, "
           f"frames/game mean {res.frames.float().mean().item():.0f} max {res.frames.max().item()}", flush=True)
+    if any(c[4:7]):  # diagnostic build: shader-clock cycles per phase, summed over workgroups
+        tot = sum(c[4:7])
+        print("   phase cycles share: A+E+B %.3f  C %.3f  D %.3f" % tuple(v / tot for v in c[4:7]), flush=True)
