@@ -29,6 +29,12 @@
  * pg_ga_select_tournament        tools.selTournament (ga.py:94; DEAP)
  * pg_ga_vary                     algorithms.varAnd with tools.cxBlend (ga.py:89)
  *                                and tools.mutGaussian (ga.py:91-92; DEAP)
+ * pg_ga_schedule                 the opponent picks of evaluate() main.py:28-66 /
+ *                                create_model_from_hall_of_fame utils.py:90-101
+ *                                for a whole population, on device
+ * pg_row_hash                    DEAP HallOfFame's similar (operator.eq on the
+ *                                gene lists, ga.py:78) as a 64-bit row hash
+ * pg_hof_update (host)           tools.HallOfFame.update (eaSimple, main.py:165-170)
  */
 #ifndef PONG_GA_H
 #define PONG_GA_H
@@ -40,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 2
+#define PG_ABI_VERSION 3
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -176,6 +182,51 @@ typedef struct pg_select_args {
   uint64_t generation;
 } pg_select_args;
 
+/* Per-game opponents of a population (evaluate(), main.py:28-66). */
+typedef enum pg_schedule_mode {
+  /* games 0, 1, 2: HardcodedAi, the ROM CPU, ScoreHardcodedAi; games >= 3: a
+   * uniformly random hall-of-fame member (create_model_from_hall_of_fame
+   * utils.py:90-101 shuffles and takes the first valid one) whose fitness is
+   * the right_score_multiplier; HardcodedAi with multiplier 1 if n_hof = 0 */
+  PG_SCHED_REFERENCE = 0,
+  /* every game against hall-of-fame row ((row_offset + i) * n_games + g) mod n_hof */
+  PG_SCHED_SELFPLAY = 1
+} pg_schedule_mode;
+
+typedef struct pg_schedule_args {
+  int32_t mode;                  /* pg_schedule_mode */
+  int32_t n;                     /* rows */
+  int32_t n_games;
+  int64_t row_offset;            /* global index of row 0 (a rank's shard) */
+  int32_t n_hof;                 /* valid hall-of-fame members: opponent rows [0, n_hof) */
+  const double *hof_fitness;     /* [n_hof] device: a pick's right_score_multiplier */
+  uint64_t seed;                 /* picks keyed by (seed, generation, global row, game) */
+  uint64_t generation;
+  int32_t *kind;                 /* out [n, n_games] device, pg_opp_kind */
+  int32_t *opp;                  /* out [n, n_games] device */
+  double *mult;                  /* out [n, n_games] device */
+} pg_schedule_args;
+
+/* HallOfFame.update (DEAP) over host arrays.  Members are in HallOfFame.items
+ * order (best first; among equal fitness the newest first); "similar" is the
+ * equality of pg_row_hash values.  Sequential semantics: an individual enters
+ * iff the hall is not full or its fitness beats the worst member strictly,
+ * and no member is similar; a full hall drops its last (worst, oldest among
+ * equals) member; an empty hall first takes population[0]. */
+typedef struct pg_hof_args {
+  int32_t maxsize;               /* HALL_OF_FAME_AMOUNT (config.py:50) */
+  int32_t hof_n;                 /* current members */
+  const double *hof_fitness;     /* [hof_n] host */
+  const uint64_t *hof_hash;      /* [hof_n] host */
+  int32_t pop_n;
+  const double *pop_fitness;     /* [pop_n] host, population order */
+  const uint64_t *pop_hash;      /* [pop_n] host */
+  int32_t *new_n;                /* out: members after the update */
+  int32_t *new_src;              /* out [maxsize]: member j's source: j' < hof_n = old member j',
+                                    hof_n + i = population row i */
+  double *new_fitness;           /* out [maxsize] */
+} pg_hof_args;
+
 const char *pg_version(void);
 int32_t pg_abi_version(void);
 const char *pg_last_error(void);
@@ -198,6 +249,13 @@ int32_t pg_ga_select_tournament(const pg_select_args *args, void *stream);
 int32_t pg_ga_select_tournament_ranked(const pg_select_args *args, const double *sorted_fitness,
                                        const int32_t *order, void *stream);
 int32_t pg_ga_vary(const pg_ga_args *args, void *stream);
+int32_t pg_ga_schedule(const pg_schedule_args *args, void *stream);
+/* hash[i] = 64-bit hash of the genes of row index[i] (row i if index is NULL):
+ * f32/f64 bit patterns, -0.0 as 0.0, so equal gene lists hash equal. */
+int32_t pg_row_hash(const void *rows, int64_t stride, const int32_t *index, int32_t n, int64_t genes,
+                    int32_t dtype, uint64_t *hash, void *stream);
+/* Host only (no device memory, no GPU needed). */
+int32_t pg_hof_update(const pg_hof_args *args);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,10 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <set>
+#include <unordered_map>
+#include <utility>
+#include <vector>
 
 #include "../../include/pong_ga.h"
 #include "pg_device.hpp"
@@ -1415,6 +1419,61 @@ __global__ void k_vary(pg_ga_args a) {
   }
 }
 
+// Opponent schedule of evaluate() (main.py:28-66) for rows [0, n).
+__global__ void k_schedule(pg_schedule_args a) {
+  const long w = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= (long)a.n * a.n_games) return;
+  const long i = w / a.n_games;
+  const int g = (int)(w % a.n_games);
+  const long row = a.row_offset + i;
+  int kind = kOppHard, opp = 0;
+  double mult = 1.0;
+  if (a.mode == PG_SCHED_SELFPLAY) {
+    if (a.n_hof > 0) {
+      kind = kOppNN;
+      opp = (int)((row * a.n_games + g) % a.n_hof);
+    }
+  } else if (g < 3) {
+    kind = g == 0 ? kOppHard : (g == 1 ? kOppRomCpu : kOppScore);
+    // right_score_multiplier is 1 until the first pick (main.py:32)
+  } else if (a.n_hof > 0) {
+    kind = kOppNN;
+    opp = (int)(u01(a.seed, a.generation, 10, (uint64_t)row, (uint64_t)g) * (double)a.n_hof);
+    opp = opp < a.n_hof ? opp : a.n_hof - 1;
+    mult = a.hof_fitness[opp];
+  }
+  a.kind[w] = kind;
+  a.opp[w] = opp;
+  a.mult[w] = mult;
+}
+
+// 64-bit content hash of each row: an order-independent sum of mixed
+// (index, bit pattern) terms, so the block reduction order cannot matter.
+template <typename WT>
+__global__ __launch_bounds__(256) void k_row_hash(const WT *rows, int64_t stride, const int32_t *index, int n,
+                                                  int64_t genes, uint64_t *out) {
+  __shared__ uint64_t part[4];
+  const int r = blockIdx.x;
+  if (r >= n) return;
+  const WT *row = rows + (long)(index ? index[r] : r) * stride;
+  uint64_t h = 0;
+  for (int64_t j = threadIdx.x; j < genes; j += 256) {
+    uint64_t bits;
+    if constexpr (sizeof(WT) == 8) {
+      const double v = row[j];
+      bits = v == 0.0 ? 0ull : (uint64_t)__double_as_longlong(v);
+    } else {
+      const float v = row[j];
+      bits = v == 0.0f ? 0ull : (uint64_t)__float_as_uint(v);
+    }
+    h += splitmix64(bits ^ ((uint64_t)j * 0x9E3779B97F4A7C15ull));
+  }
+  for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) out[r] = splitmix64(part[0] + part[1] + part[2] + part[3] + (uint64_t)genes);
+}
+
 // ====================================================== host dispatch ====
 static int gene_count(const pg_net &n) {
   const int b = n.bias ? 1 : 0;
@@ -1810,6 +1869,88 @@ int32_t pg_ga_vary(const pg_ga_args *a, void *stream) {
   else
     hipLaunchKernelGGL(k_vary<float>, grid, dim3(256), 0, (hipStream_t)stream, *a);
   PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_ga_schedule(const pg_schedule_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  if (a->n < 0 || a->n_games < 1 || a->n_hof < 0 || a->row_offset < 0 ||
+      (a->mode != PG_SCHED_REFERENCE && a->mode != PG_SCHED_SELFPLAY))
+    return fail(PG_ERR_INVALID, "schedule: bad sizes or mode");
+  if (a->n == 0) return PG_OK;
+  if (!a->kind || !a->opp || !a->mult || (a->mode == PG_SCHED_REFERENCE && a->n_hof > 0 && !a->hof_fitness))
+    return fail(PG_ERR_INVALID, "schedule: NULL output or hof_fitness");
+  const long total = (long)a->n * a->n_games;
+  hipLaunchKernelGGL(k_schedule, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *a);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_row_hash(const void *rows, int64_t stride, const int32_t *index, int32_t n, int64_t genes,
+                    int32_t dtype, uint64_t *hash, void *stream) {
+  if (n < 0 || genes < 0 || (n > 0 && (!rows || !hash || stride < genes)) || (dtype != PG_F32 && dtype != PG_F64))
+    return fail(PG_ERR_INVALID, "row_hash: bad sizes, dtype or NULL buffers");
+  if (n == 0) return PG_OK;
+  if (dtype == PG_F64)
+    hipLaunchKernelGGL(k_row_hash<double>, dim3(n), dim3(256), 0, (hipStream_t)stream, (const double *)rows, stride,
+                       index, n, genes, hash);
+  else
+    hipLaunchKernelGGL(k_row_hash<float>, dim3(n), dim3(256), 0, (hipStream_t)stream, (const float *)rows, stride,
+                       index, n, genes, hash);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_hof_update(const pg_hof_args *a) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  if (a->maxsize < 0 || a->hof_n < 0 || a->hof_n > a->maxsize || a->pop_n < 0 || !a->new_n ||
+      (a->maxsize > 0 && (!a->new_src || !a->new_fitness)) || (a->hof_n > 0 && (!a->hof_fitness || !a->hof_hash)) ||
+      (a->pop_n > 0 && (!a->pop_fitness || !a->pop_hash)))
+    return fail(PG_ERR_INVALID, "hof_update: bad sizes or NULL buffers");
+  // members ordered as HallOfFame.keys: (fitness ascending, insertion order ascending);
+  // items order is the reverse.  seq: later insertions compare greater.
+  struct Member {
+    double fit;
+    long seq;
+    int src;
+    uint64_t hash;
+    bool operator<(const Member &o) const { return fit < o.fit || (fit == o.fit && seq < o.seq); }
+  };
+  std::set<Member> hof;
+  std::unordered_map<uint64_t, int> hashes;  // hash -> members holding it
+  long seq = 0;
+  // existing members, given best first (items order): insert worst first
+  for (int j = a->hof_n - 1; j >= 0; --j) {
+    hof.insert({a->hof_fitness[j], seq++, j, a->hof_hash[j]});
+    hashes[a->hof_hash[j]] += 1;
+  }
+  auto insert = [&](int i) {
+    hof.insert({a->pop_fitness[i], seq++, a->hof_n + i, a->pop_hash[i]});
+    hashes[a->pop_hash[i]] += 1;
+  };
+  for (int i = 0; i < a->pop_n; ++i) {
+    if (hof.empty() && a->maxsize != 0) {  // DEAP: an empty hall takes population[0]
+      insert(0);
+      continue;
+    }
+    if (a->maxsize == 0) continue;
+    const double f = a->pop_fitness[i];
+    const bool better = f > hof.begin()->fit;  // ind.fitness > self[-1].fitness
+    if (!(better || (int)hof.size() < a->maxsize)) continue;
+    if (hashes.count(a->pop_hash[i]) && hashes[a->pop_hash[i]] > 0) continue;  // similar to a member
+    if ((int)hof.size() >= a->maxsize) {  // remove(-1): the worst, oldest among equal keys
+      auto worst = hof.begin();
+      hashes[worst->hash] -= 1;
+      hof.erase(worst);
+    }
+    insert(i);
+  }
+  int j = 0;
+  for (auto it = hof.rbegin(); it != hof.rend(); ++it, ++j) {
+    a->new_src[j] = it->src;
+    a->new_fitness[j] = it->fit;
+  }
+  *a->new_n = j;
   return PG_OK;
 }
 

@@ -16,13 +16,14 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 2
+PG_ABI_VERSION = 3
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
 PG_F32, PG_F64 = 0, 1
 PG_OPP_HARDCODED, PG_OPP_ROM_CPU, PG_OPP_SCORE, PG_OPP_NN = 0, 1, 2, 3
 PG_PREC_CERTIFIED, PG_PREC_F64 = 0, 1
+PG_SCHED_REFERENCE, PG_SCHED_SELFPLAY = 0, 1
 PG_KERNEL_AUTO, PG_KERNEL_GENERAL, PG_KERNEL_RESIDENT, PG_KERNEL_SPLIT, PG_KERNEL_WIDE = 0, 1, 2, 3, 4
 PG_STATE_FIELDS = 16
 STATE_FIELD_NAMES = ("ball_x", "ball_y", "ball_vx", "ball_vy", "ball_visible", "serve_timer",
@@ -80,6 +81,23 @@ class PgSelectArgs(ctypes.Structure):
     ]
 
 
+class PgScheduleArgs(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int32), ("n", ctypes.c_int32), ("n_games", ctypes.c_int32),
+        ("row_offset", ctypes.c_int64), ("n_hof", ctypes.c_int32), ("hof_fitness", _vp),
+        ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64),
+        ("kind", _vp), ("opp", _vp), ("mult", _vp),
+    ]
+
+
+class PgHofArgs(ctypes.Structure):
+    _fields_ = [
+        ("maxsize", ctypes.c_int32), ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("hof_hash", _vp),
+        ("pop_n", ctypes.c_int32), ("pop_fitness", _vp), ("pop_hash", _vp),
+        ("new_n", _vp), ("new_src", _vp), ("new_fitness", _vp),
+    ]
+
+
 # name -> (restype, argtypes); exactly the functions include/pong_ga.h declares
 SIGNATURES = {
     "pg_version": (ctypes.c_char_p, []),
@@ -95,6 +113,10 @@ SIGNATURES = {
     "pg_ga_select_tournament": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp]),
     "pg_ga_select_tournament_ranked": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp, _vp, _vp]),
     "pg_ga_vary": (ctypes.c_int32, [ctypes.POINTER(PgGaArgs), _vp]),
+    "pg_ga_schedule": (ctypes.c_int32, [ctypes.POINTER(PgScheduleArgs), _vp]),
+    "pg_row_hash": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp,
+                                     _vp]),
+    "pg_hof_update": (ctypes.c_int32, [ctypes.POINTER(PgHofArgs)]),
 }
 
 _lock = threading.Lock()

@@ -273,3 +273,65 @@ def vary(parents: torch.Tensor, chosen: torch.Tensor, genes: int, cxpb: float, m
     with torch.cuda.device(dev):
         L.check("pg_ga_vary", L.lib().pg_ga_vary(ctypes.byref(a), _stream(dev)))
     return out, invalid
+
+
+SCHEDULES = {"reference": L.PG_SCHED_REFERENCE, "selfplay": L.PG_SCHED_SELFPLAY}
+
+
+def schedule(mode: str, n: int, n_games: int, row_offset: int, hof_fitness: Optional[torch.Tensor], n_hof: int,
+             seed: int, generation: int, device):
+    """pg_ga_schedule: (kind, opp, mult) [n, n_games] of evaluate()'s games on device."""
+    dev = torch.device(device)
+    kind = torch.empty((n, n_games), dtype=torch.int32, device=dev)
+    opp = torch.empty((n, n_games), dtype=torch.int32, device=dev)
+    mult = torch.empty((n, n_games), dtype=torch.float64, device=dev)
+    if hof_fitness is not None:
+        _need(hof_fitness, "hof_fitness", torch.float64, dev)
+        if hof_fitness.numel() < n_hof:
+            raise ValueError(f"hof_fitness holds {hof_fitness.numel()} values, n_hof={n_hof}")
+    elif n_hof and mode == "reference":
+        raise ValueError("reference schedule with a hall of fame needs hof_fitness")
+    a = L.PgScheduleArgs(SCHEDULES[mode], n, n_games, row_offset, n_hof, _ptr(hof_fitness), seed, generation,
+                         _ptr(kind), _ptr(opp), _ptr(mult))
+    with torch.cuda.device(dev):
+        L.check("pg_ga_schedule", L.lib().pg_ga_schedule(ctypes.byref(a), _stream(dev)))
+    return kind, opp, mult
+
+
+def row_hash(rows: torch.Tensor, genes: Optional[int] = None, index: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """pg_row_hash: int64 (the uint64 bits) content hash of each row's first
+    ``genes`` genes, for every row or for the rows ``index`` names."""
+    if rows.dim() != 2 or rows.dtype not in DTYPES or rows.stride(1) != 1:
+        raise ValueError("rows must be a row-major [n, G] f32/f64 tensor")
+    genes = rows.shape[1] if genes is None else int(genes)
+    n = rows.shape[0] if index is None else index.shape[0]
+    if index is not None:
+        _need(index, "index", torch.int32, rows.device, (n,))
+    out = torch.empty(n, dtype=torch.int64, device=rows.device)
+    stride = rows.stride(0) if rows.shape[0] > 1 else rows.shape[1]
+    with torch.cuda.device(rows.device):
+        L.check("pg_row_hash", L.lib().pg_row_hash(_ptr(rows), stride, _ptr(index), n, genes, DTYPES[rows.dtype],
+                                                   _ptr(out), _stream(rows.device)))
+    return out
+
+
+def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash):
+    """pg_hof_update (host, no GPU): HallOfFame.update over fitness/hash arrays.
+
+    Returns (src [new_n] int32, fitness [new_n] f64): member j comes from old
+    member src[j] if src[j] < len(hof_fitness), else from population entry
+    src[j] - len(hof_fitness)."""
+    import numpy as np
+    hf = np.ascontiguousarray(hof_fitness, dtype=np.float64)
+    hh = np.ascontiguousarray(np.asarray(hof_hash, dtype=np.int64)).view(np.uint64)
+    pf = np.ascontiguousarray(pop_fitness, dtype=np.float64)
+    ph = np.ascontiguousarray(np.asarray(pop_hash, dtype=np.int64)).view(np.uint64)
+    if hf.shape != hh.shape or pf.shape != ph.shape:
+        raise ValueError("fitness and hash arrays must pair up")
+    src = np.zeros(max(maxsize, 1), dtype=np.int32)
+    fit = np.zeros(max(maxsize, 1), dtype=np.float64)
+    new_n = ctypes.c_int32(0)
+    a = L.PgHofArgs(maxsize, hf.shape[0], hf.ctypes.data, hh.ctypes.data, pf.shape[0], pf.ctypes.data,
+                    ph.ctypes.data, ctypes.addressof(new_n), src.ctypes.data, fit.ctypes.data)
+    L.check("pg_hof_update", L.lib().pg_hof_update(ctypes.byref(a)))
+    return src[: new_n.value].copy(), fit[: new_n.value].copy()
