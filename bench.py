@@ -9,8 +9,9 @@ One step = one GA generation of the reference's eaSimple loop
   1. evaluate every genome's 6 self-play games to termination
      (pg_eval_population: Pong physics + both paddles' [6,64,3] MLPs, fused),
   2. all-gather the fitness over ranks (RCCL; N > 1 only),
-  3. hall-of-fame update (top pop//4 of HoF + population),
-  4. selTournament(tournsize = pop//4) + varAnd(cxBlend, mutGaussian) on device.
+  3. HallOfFame.update (DEAP semantics: pg_row_hash on device, pg_hof_update on the host),
+  4. selTournament(tournsize = pop//4) + varAnd(cxBlend, mutGaussian) on device
+(pong_amd.evolve.DeviceGA, the product's device-resident eaSimple).
 Weak scaling: every rank evaluates 65 536 genomes of an N x 65 536 population.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 through
@@ -80,7 +81,7 @@ def main():
 
     from pong_amd import build as B
     from pong_amd import device as D
-    from pong_amd import dist as PD
+    from pong_amd.evolve import DeviceGA
     B.build()
 
     shape = [int(v) for v in args.shape.split(",")]
@@ -89,55 +90,29 @@ def main():
     P = n_local * world
     H = max(P // 4, 1)                 # HALL_OF_FAME_AMOUNT = POPULATION_SIZE // 4 (config.py:49-50)
     tournsize = max(P // 4, 1)          # TOURNAMENT_SIZE (config.py:49)
-    ev = D.Evaluator(shape, dtype=dtype, device=dev, n_games=args.games, kernel=args.kernel,
-                     group_lanes=args.group_lanes)
-    G = ev.genes
+    # the device-resident eaSimple (pong_amd.evolve): replicated population,
+    # rank r evaluates its shard, one all-gather of fitness per generation;
+    # GA parameters are config.py's (cxpb = mutpb = indpb = alpha = sigma = 0.9, mu = 0)
+    ga = DeviceGA(shape, P, H, tournsize, dtype=dtype, device=dev, n_games=args.games, schedule="selfplay",
+                  seed=args.seed, kernel=args.kernel)
+    ga.ev.group_lanes = args.group_lanes
+    G = ga.G
+    ga.initialize("normal", args.sigma)
+    # the first games already face a full hall of fame: H independent random
+    # genomes at fitness -1e300, which the first update replaces
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 1)
+    rows = max(1, (1 << 28) // (8 * G))
+    for r0 in range(0, H, rows):
+        r1 = min(H, r0 + rows)
+        ga.store[r0:r1] = torch.randn((r1 - r0, G), generator=gen, dtype=torch.float64,
+                                      device=dev).mul_(args.sigma).to(dtype)
+    ga.set_hall_of_fame(None, np.full(H, -1e300))
+    lo = ga.lo
 
-    # replicated population (identical on every rank: same seed), HoF = first H genomes.
-    # Storage [H + P, G]: rows [0, H) the hall of fame, rows [H, H + P) the
-    # population, so the HoF candidates (HoF + population) are one gather.
-    gen = torch.Generator(device=dev).manual_seed(args.seed)
-    store = torch.empty((H + P, G), dtype=dtype, device=dev)
-    rows = max(1, (1 << 30) // (8 * G))  # draw in ~1 GB chunks (the wide population is 70 GB in f32)
-    for r0 in range(0, P, rows):
-        r1 = min(P, r0 + rows)
-        store[H + r0:H + r1] = torch.randn((r1 - r0, G), generator=gen, dtype=torch.float64,
-                                           device=dev).mul_(args.sigma).to(dtype)
-    store[:H] = store[H:H + H]
-    spare = torch.empty_like(store)
-    hof_fit = torch.full((H,), -1e300, dtype=torch.float64, device=dev)
-    lo, hi = PD.shard_range(P, rank, world)
-    kind, opp, mult = ev.selfplay_schedule(hi - lo, H, offset=lo)
-    res_buf = None
-
-    cxpb, mutpb, alpha, mu, sigma, indpb = 0.9, 0.9, 0.9, 0.0, 0.9, 0.9  # config.py:36-42
     ev_start = torch.cuda.Event(enable_timing=True)
     ev_end = torch.cuda.Event(enable_timing=True)
-
-    def generation(g, timed):
-        nonlocal store, spare, hof_fit, res_buf
-        hof, pop = store[:H], store[H:]
-        if timed:
-            ev_start.record()
-        res, _ = ev.evaluate(pop[lo:hi], kind, opp, mult, opponents=hof, out=res_buf, validate=False)
-        if timed:
-            ev_end.record()
-        res_buf = res
-        fit = PD.gather_fitness(res.fitness, P) if world > 1 else res.fitness
-        # hall of fame: best H of (HoF, population), gathered into the next storage
-        cand = torch.cat([hof_fit, fit])
-        top = torch.topk(cand, H, sorted=False).indices
-        torch.index_select(store, 0, top, out=spare[:H])
-        hof_fit = cand[top]
-        # selection + variation: offspring into the next storage's population rows
-        chosen = D.select_tournament_ranked(fit, P, tournsize, seed=args.seed, generation=g)
-        D.vary(pop, chosen, G, cxpb, mutpb, alpha, mu, sigma, indpb, seed=args.seed,
-               generation=g, out=spare[H:])
-        store, spare = spare, store
-        return res
-
     for w in range(args.warmup):
-        generation(w, False)
+        ga.step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -150,13 +125,14 @@ def main():
     passes_local = 0        # k_wide: network weight passes (each streams one network's genes once)
     kernel_ms = []
     counters = []
+    ga.eval_events = (ev_start, ev_end)
     for s in range(args.steps):
-        res = generation(args.warmup + s, True)
-        counters.append(res.counters.clone())
-        kernel_ms.append((ev_start, ev_end))
+        ga.step()  # evaluate + all-gather + hall of fame + select + vary (one generation)
+        counters.append(ga.last.counters.clone())
         # events are reused: read this step's kernel time before the next record
         torch.cuda.synchronize(dev)
-        kernel_ms[-1] = ev_start.elapsed_time(ev_end)
+        kernel_ms.append(ev_start.elapsed_time(ev_end))
+    ga.eval_events = None
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -193,7 +169,7 @@ def main():
         out = wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all,
                           passes_all, kernel_ms_mean)
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args, shape, store[H:], store[:H], kind, opp, mult, lo, chunk=8,
+            out["cpu_baseline"] = cpu_baseline(args, shape, ga, chunk=8,
                                               max_rows=256)
         print(json.dumps(out), flush=True)
     elif rank == 0:
@@ -246,7 +222,7 @@ def main():
                          "streaming_equivalent_frac_of_hbm": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9 / HBM_PEAK_GBS},
         }
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args, shape, store[H:], store[:H], kind, opp, mult, lo)
+            out["cpu_baseline"] = cpu_baseline(args, shape, ga)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -301,15 +277,21 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
     }
 
 
-def cpu_baseline(args, shape, pop, hof, kind, opp, mult, lo, chunk=256, max_rows=1 << 16):
+def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16):
     """The CPU oracle (C restatement of the reference loop, f64 numpy_nn
-    arithmetic) on the same workload's first genomes, on the host cores."""
+    arithmetic) on the same workload's first genomes (this rank's population
+    rows against the current hall of fame), on the host cores."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
+    from pong_amd import device as D
     O.build()
-    genomes = pop[lo:lo + max_rows].double().cpu().numpy()
+    lo = ga.lo
+    genomes = ga.population[lo:lo + max_rows].double().cpu().numpy()
     n = genomes.shape[0]
-    k, o, m = kind[:n].cpu().numpy(), opp[:n].cpu().numpy(), mult[:n].cpu().numpy()
+    kind, opp, mult = D.schedule(ga.schedule, n, ga.n_games, lo, ga.hof_fitness, ga.hof_n, ga.seed,
+                                 ga.generation + 1, ga.device)
+    hof = ga.hall_of_fame
+    k, o, m = kind.cpu().numpy(), opp.cpu().numpy(), mult.cpu().numpy()
     # only the hall-of-fame rows these genomes play (the wide HoF is 35 GB in f64)
     rows = np.unique(o)
     opponents = hof[torch.as_tensor(rows, device=hof.device)].double().cpu().numpy()

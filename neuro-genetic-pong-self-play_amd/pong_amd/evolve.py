@@ -1,0 +1,270 @@
+"""Device-resident eaSimple: the reference's GA loop (main.py:157-173, which
+runs DEAP's ``algorithms.eaSimple`` with the operators ga.py:76-94 registers)
+with every per-individual step on the MI355X.
+
+One generation (eaSimple, gen >= 1):
+
+====================================================  =========================================
+offspring = varAnd(selTournament(pop, len(pop)))      pg_ga_select_tournament_ranked + pg_ga_vary
+evaluate the invalid offspring (evaluate, main.py:28)  pg_ga_schedule + pg_eval_population
+halloffame.update(offspring)                           pg_row_hash (device) + pg_hof_update (host)
+population[:] = offspring; record avg/std/min/max      main.py:158-162 statistics
+====================================================  =========================================
+
+Generation 0 evaluates the initial population and fills the hall of fame.
+
+Storage: one ``[H + P, G]`` buffer, hall-of-fame rows first, and a spare of
+the same shape that the next generation is written into, so neither the
+variation nor the hall-of-fame gather reads what it writes.  The GA state is
+replicated on every rank; rank r evaluates rows ``shard_range(P, r, N)`` and
+the fitness vector is all-gathered once per generation -- the only collective.
+
+Differences from DEAP (DESIGN.md "GA"): random draws are counter-based
+(distribution parity, not Mersenne-Twister stream parity); ``similar`` is the
+equality of 64-bit gene hashes; unmodified offspring keep their parent's
+fitness as DEAP's clones do (the batched launch plays their games too and the
+result is discarded).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import device as D
+from . import dist as PD
+
+STAT_FIELDS = ("avg", "std", "min", "max")  # main.py:159-162
+
+
+class DeviceGA:
+    """eaSimple state on one device (one per rank): population, fitness, hall of fame, logbook."""
+
+    def __init__(self, nodes, population_size: int, hof_size: Optional[int] = None,
+                 tournsize: Optional[int] = None, *, bias: bool = True, dtype=torch.float64, device=None,
+                 n_games: int = 6, schedule: str = "reference", cxpb: float = 0.9, mutpb: float = 0.9,
+                 alpha: float = 0.9, mu: float = 0.0, sigma: float = 0.9, indpb: float = 0.9,
+                 seed: int = 0, physics_seed: int = 0, precision: str = "certified", kernel: str = "auto",
+                 group=None):
+        if schedule not in D.SCHEDULES:
+            raise ValueError(f"schedule must be one of {sorted(D.SCHEDULES)}")
+        self.nodes = [int(v) for v in nodes]
+        self.P = int(population_size)
+        # HALL_OF_FAME_AMOUNT = TOURNAMENT_SIZE = POPULATION_SIZE // 4 (config.py:49-50)
+        self.H = int(hof_size) if hof_size is not None else max(self.P // 4, 1)
+        self.tournsize = int(tournsize) if tournsize is not None else max(self.P // 4, 1)
+        if self.P < 1 or self.H < 0 or self.tournsize < 1:
+            raise ValueError("population_size >= 1, hof_size >= 0 and tournsize >= 1 required")
+        self.ev = D.Evaluator(self.nodes, bias=bias, dtype=dtype, device=device, n_games=n_games,
+                              precision=precision, kernel=kernel, seed=physics_seed)
+        self.device, self.dtype, self.G = self.ev.device, dtype, self.ev.genes
+        self.bias, self.n_games, self.schedule = bool(bias), int(n_games), schedule
+        self.cxpb, self.mutpb, self.alpha = float(cxpb), float(mutpb), float(alpha)
+        self.mu, self.sigma, self.indpb = float(mu), float(sigma), float(indpb)
+        self.seed, self.physics_seed = int(seed), int(physics_seed)
+        self.precision, self.kernel = precision, kernel
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.lo, self.hi = PD.shard_range(self.P, self.rank, self.world)
+        self.store = torch.zeros((self.H + self.P, self.G), dtype=dtype, device=self.device)
+        self.spare = torch.empty_like(self.store)
+        self.fitness = torch.zeros(self.P, dtype=torch.float64, device=self.device)
+        self.valid = torch.zeros(self.P, dtype=torch.bool, device=self.device)
+        self.hof_fitness = torch.zeros(max(self.H, 1), dtype=torch.float64, device=self.device)
+        self.hof_n = 0
+        self._hof_fit_host = np.zeros(0, np.float64)   # HallOfFame.items order (best first)
+        self._hof_hash_host = np.zeros(0, np.int64)
+        self.generation = -1  # -1: the initial population is not evaluated yet
+        self.logbook = []
+        self.last = None       # EvalResult of the latest evaluation (this rank's rows)
+        self.eval_events = None  # optional (start, end) HIP events recorded around the evaluation launch
+
+    # ------------------------------------------------------------ views
+    @property
+    def population(self) -> torch.Tensor:
+        return self.store[self.H:]
+
+    @property
+    def hall_of_fame(self) -> torch.Tensor:
+        """Members, best first (HallOfFame.items order)."""
+        return self.store[: self.hof_n]
+
+    @property
+    def hof_member_fitness(self) -> np.ndarray:
+        return self._hof_fit_host.copy()
+
+    # ------------------------------------------------------------ state
+    def initialize(self, init: str = "uniform", init_sigma: float = 3.0):
+        """toolbox.population(n=P): genes U[0,1) as toolbox.attr_float = random.random
+        (ga.py:85), or N(0, init_sigma) ("normal"), drawn on device in row blocks."""
+        gen = torch.Generator(device=self.device).manual_seed(self.seed)
+        rows = max(1, (1 << 28) // (8 * self.G))
+        for r0 in range(0, self.P, rows):
+            r1 = min(self.P, r0 + rows)
+            if init == "uniform":
+                blk = torch.rand((r1 - r0, self.G), generator=gen, dtype=torch.float64, device=self.device)
+            elif init == "normal":
+                blk = torch.randn((r1 - r0, self.G), generator=gen, dtype=torch.float64,
+                                  device=self.device).mul_(init_sigma)
+            else:
+                raise ValueError("init must be 'uniform' or 'normal'")
+            self.store[self.H + r0:self.H + r1] = blk.to(self.dtype)
+        self.valid.zero_()
+        self.fitness.zero_()
+        self._set_hof_empty()
+        self.generation = -1
+        self.logbook = []
+
+    def set_population(self, genomes: torch.Tensor, fitness: Optional[torch.Tensor] = None,
+                       valid: Optional[torch.Tensor] = None):
+        """Load P genomes (and, for individuals whose fitness is valid, their fitness)."""
+        if tuple(genomes.shape) != (self.P, self.G):
+            raise ValueError(f"genomes must be [{self.P}, {self.G}], got {tuple(genomes.shape)}")
+        self.population.copy_(genomes.to(device=self.device, dtype=self.dtype))
+        if fitness is None:
+            self.valid.zero_()
+            self.fitness.zero_()
+        else:
+            self.fitness.copy_(fitness.to(device=self.device, dtype=torch.float64))
+            v = torch.ones(self.P, dtype=torch.bool) if valid is None else valid.to(torch.bool)
+            self.valid.copy_(v.to(self.device))
+
+    def set_hall_of_fame(self, genomes: Optional[torch.Tensor], fitness):
+        """Load hall-of-fame members, best first (HallOfFame.items order);
+        ``genomes`` None: the members were written into hall-of-fame rows
+        ``store[:n]`` in place."""
+        fit = np.asarray(fitness, dtype=np.float64)
+        n = fit.shape[0]
+        if n > self.H or (genomes is not None and tuple(genomes.shape) != (n, self.G)):
+            raise ValueError(f"hall of fame must be [<= {self.H}, {self.G}] with matching fitness")
+        if n and np.any(np.diff(fit) > 0):
+            raise ValueError("hall-of-fame members must be ordered best first")
+        if genomes is not None:
+            self.store[:n] = genomes.to(device=self.device, dtype=self.dtype)
+        self.hof_n = n
+        self._hof_fit_host = fit.copy()
+        self._hof_hash_host = D.row_hash(self.store[:n], self.G).cpu().numpy() if n else np.zeros(0, np.int64)
+        if n:
+            self.hof_fitness[:n] = torch.from_numpy(fit).to(self.device)
+
+    def _set_hof_empty(self):
+        self.hof_n = 0
+        self._hof_fit_host = np.zeros(0, np.float64)
+        self._hof_hash_host = np.zeros(0, np.int64)
+
+    # ------------------------------------------------------------ steps
+    def _evaluate(self, g: int, rows: torch.Tensor) -> torch.Tensor:
+        """Fitness of every row of ``rows`` ([P, G]): this rank plays its shard's
+        games, then the fitness vector is all-gathered."""
+        n = self.hi - self.lo
+        kind, opp, mult = D.schedule(self.schedule, n, self.n_games, self.lo, self.hof_fitness, self.hof_n,
+                                     self.seed, g, self.device)
+        opponents = self.store[: self.hof_n] if self.hof_n else None
+        out = self.last if (self.last is not None and self.last.fitness.shape[0] == n) else None
+        if self.eval_events is not None:
+            self.eval_events[0].record()
+        res, _ = self.ev.evaluate(rows[self.lo:self.hi], kind, opp, mult, opponents=opponents, out=out,
+                                  validate=False)
+        if self.eval_events is not None:
+            self.eval_events[1].record()
+        self.last = res
+        return PD.gather_fitness(res.fitness, self.P, self.group) if self.world > 1 else res.fitness
+
+    @staticmethod
+    def _check(fit: torch.Tensor):
+        # a NaN fitness is a game whose calculate_reward divided by zero (utils.py:106-108)
+        if bool(torch.isnan(fit).any()):
+            raise ZeroDivisionError("float division by zero (calculate_reward with total_frames == 0)")
+
+    def _hof_update(self, fit: torch.Tensor, rows: torch.Tensor, dst: torch.Tensor):
+        """HallOfFame.update(rows) with fitness ``fit``; the members are gathered
+        into dst[:new_n] (dst is disjoint from the current members and rows)."""
+        if self.H == 0:
+            return
+        old_n = self.hof_n
+        if old_n >= self.H:
+            # a full hall only admits fitness > its worst, and the worst only rises:
+            # rows at or below today's worst can never enter
+            cand = torch.nonzero(fit > float(self._hof_fit_host[-1])).flatten()
+        else:
+            cand = torch.arange(self.P, device=self.device)
+        k = int(cand.numel())
+        if k == 0:
+            dst[:old_n] = self.store[:old_n]
+            return
+        cand32 = cand.to(torch.int32)
+        h = D.row_hash(rows, self.G, index=cand32).cpu().numpy()
+        f = fit[cand].cpu().numpy()
+        src, new_fit = D.hof_update(self.H, self._hof_fit_host, self._hof_hash_host, f, h)
+        is_old = src < old_n
+        src_t = torch.from_numpy(src.astype(np.int64)).to(self.device)
+        old_t = torch.from_numpy(is_old).to(self.device)
+        pos = torch.arange(src.shape[0], device=self.device)
+        if is_old.any():
+            dst[pos[old_t]] = self.store[src_t[old_t]]
+        if (~is_old).any():
+            dst[pos[~old_t]] = rows[cand[src_t[~old_t] - old_n]]
+        hashes = np.empty(src.shape[0], np.int64)
+        hashes[is_old] = self._hof_hash_host[src[is_old]]
+        hashes[~is_old] = h[src[~is_old] - old_n]
+        self.hof_n = int(src.shape[0])
+        self._hof_fit_host, self._hof_hash_host = new_fit, hashes
+        self.hof_fitness[: self.hof_n] = torch.from_numpy(new_fit).to(self.device)
+
+    def _record(self, g: int, nevals: int) -> dict:
+        f = self.fitness
+        vals = torch.stack([f.mean(), f.std(unbiased=False), f.min(), f.max()]).tolist()
+        rec = {"gen": g, "nevals": nevals, **dict(zip(STAT_FIELDS, vals))}
+        self.logbook.append(rec)
+        return rec
+
+    def step(self) -> dict:
+        """One eaSimple generation (or, first, the initial evaluation); returns the logbook row."""
+        if self.generation < 0:
+            fit = self._evaluate(0, self.population)
+            nevals = int((~self.valid).sum())
+            new_fit = torch.where(self.valid, self.fitness, fit)
+            self._check(new_fit)
+            self.fitness, self.valid = new_fit, torch.ones_like(self.valid)
+            self._hof_update(new_fit, self.population, self.spare)
+            self.store[: self.hof_n] = self.spare[: self.hof_n]
+            self.generation = 0
+            return self._record(0, nevals)
+        g = self.generation + 1
+        chosen = D.select_tournament_ranked(self.fitness, self.P, self.tournsize, seed=self.seed, generation=g)
+        off = self.spare[self.H:]
+        _, invalid = D.vary(self.population, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu,
+                            self.sigma, self.indpb, seed=self.seed, generation=g, out=off)
+        inv = invalid.bool()
+        inherited = self.fitness[chosen.long()]  # a clone keeps its parent's fitness (varAnd)
+        fit = self._evaluate(g, off)
+        new_fit = torch.where(inv, fit, inherited)
+        self._check(new_fit)
+        self._hof_update(new_fit, off, self.spare)
+        self.fitness = new_fit
+        self.store, self.spare = self.spare, self.store
+        self.generation = g
+        return self._record(g, int(inv.sum()))
+
+    def run(self, ngen: int, verbose: bool = False) -> list:
+        """algorithms.eaSimple(..., ngen): the initial evaluation if pending, then ngen generations."""
+        rows = []
+        if self.generation < 0:
+            rows.append(self.step())
+            if verbose:
+                _print_row(rows[-1], header=True)
+        for _ in range(int(ngen)):
+            rows.append(self.step())
+            if verbose:
+                _print_row(rows[-1], header=False)
+        return rows
+
+
+def _print_row(rec: dict, header: bool):
+    cols = ("gen", "nevals") + STAT_FIELDS
+    if header:
+        print("\t".join(cols))
+    print("\t".join(str(rec[c]) for c in cols))

@@ -1,0 +1,80 @@
+"""pg_hof_update (host C++ in libpong_ga.so, no GPU) against the DEAP
+HallOfFame restatement (pong_amd.deap_compat.tools.HallOfFame, DEAP's
+published algorithm; deap itself is absent offline, so parity is unpinned
+beyond the restatement).  Individuals are one-gene lists whose gene is the
+row hash, so DEAP's ``similar`` (operator.eq on the gene lists) is exactly
+hash equality."""
+import random
+
+import numpy as np
+import pytest
+
+from pong_amd import device as D
+from pong_amd.deap_compat import base, creator, tools
+
+
+@pytest.fixture(scope="module")
+def Ind():
+    if not hasattr(creator, "HofFitness"):
+        creator.create("HofFitness", base.Fitness, weights=(1.0,))
+        creator.create("HofInd", list, fitness=creator.HofFitness)
+    return creator.HofInd
+
+
+def _mk(Ind, h, f):
+    ind = Ind([int(h)])
+    ind.fitness.values = (float(f),)
+    return ind
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_hof_update_matches_deap_restatement(Ind, seed):
+    rng = np.random.default_rng(seed)
+    maxsize = int(rng.integers(1, 24))
+    hof = tools.HallOfFame(maxsize)
+    keys_f, keys_h = np.zeros(0), np.zeros(0, np.int64)
+    for _ in range(6):  # successive generations
+        n = int(rng.integers(0, 60))
+        # few distinct fitness values (ties) and few distinct genes (duplicates)
+        fit = rng.integers(0, 8, size=n).astype(np.float64) * 0.5
+        hsh = rng.integers(-2**62, 2**62, size=8)[rng.integers(0, 8, size=n)]
+        pop = [_mk(Ind, h, f) for h, f in zip(hsh, fit)]
+        hof.update(pop)
+        src, new_fit = D.hof_update(maxsize, keys_f, keys_h, fit, hsh)
+        old_n = keys_f.shape[0]
+        new_h = np.array([keys_h[s] if s < old_n else hsh[s - old_n] for s in src], dtype=np.int64)
+        assert [i.fitness.values[0] for i in hof] == list(new_fit)
+        assert [i[0] for i in hof] == list(new_h)
+        keys_f, keys_h = new_fit, new_h
+
+
+def test_hof_update_edge_cases(Ind):
+    # empty population, maxsize 0, an empty hall taking population[0] first
+    src, fit = D.hof_update(4, [], [], [], [])
+    assert len(src) == 0
+    src, fit = D.hof_update(0, [], [], [1.0, 2.0], [1, 2])
+    assert len(src) == 0
+    src, fit = D.hof_update(2, [], [], [1.0, 5.0, 5.0, 3.0], [7, 7, 8, 9])
+    hof = tools.HallOfFame(2)
+    hof.update([_mk(Ind, h, f) for h, f in zip([7, 7, 8, 9], [1.0, 5.0, 5.0, 3.0])])
+    assert list(fit) == [i.fitness.values[0] for i in hof]
+    assert list(src) == [2, 3]  # [8] at 5.0 then [9] at 3.0; [7] at 5.0 was similar to [7] at 1.0
+
+
+def test_hof_update_rejects_bad_arguments():
+    from pong_amd import _lib
+    with pytest.raises(_lib.PongGAError):
+        D.hof_update(1, [1.0, 2.0], [1, 2], [], [])  # more members than maxsize
+    with pytest.raises(ValueError):
+        D.hof_update(3, [1.0], [], [], [])
+
+
+def test_hof_update_large_is_fast():
+    import time
+    rng = np.random.default_rng(0)
+    n, H = 65536, 16384
+    t0 = time.perf_counter()
+    src, fit = D.hof_update(H, [], [], rng.standard_normal(n), rng.integers(-2**62, 2**62, size=n))
+    assert len(src) == H and np.all(np.diff(fit) <= 0)
+    assert time.perf_counter() - t0 < 1.0
+    random.seed(0)
