@@ -61,7 +61,8 @@ def parse():
     wide = a.config == "wide"
     # presets: a wide generation takes ~30 s at 65 536 genomes, so fewer steps
     a.steps = a.steps if a.steps is not None else (1 if wide else 5)
-    a.warmup = a.warmup if a.warmup is not None else (0 if wide else 1)
+    # two warm-up steps: the initial evaluation and one full generation (first-call costs of select/vary)
+    a.warmup = a.warmup if a.warmup is not None else (0 if wide else 2)
     a.shape = a.shape or ("6,512,512,3" if wide else "6,64,3")
     a.dtype = a.dtype or ("float32" if wide else "float64")
     return a

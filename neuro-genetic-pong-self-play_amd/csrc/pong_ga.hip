@@ -24,7 +24,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
-#include <set>
+#include <algorithm>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -1907,50 +1907,71 @@ int32_t pg_hof_update(const pg_hof_args *a) {
       (a->maxsize > 0 && (!a->new_src || !a->new_fitness)) || (a->hof_n > 0 && (!a->hof_fitness || !a->hof_hash)) ||
       (a->pop_n > 0 && (!a->pop_fitness || !a->pop_hash)))
     return fail(PG_ERR_INVALID, "hof_update: bad sizes or NULL buffers");
-  // members ordered as HallOfFame.keys: (fitness ascending, insertion order ascending);
-  // items order is the reverse.  seq: later insertions compare greater.
+  // Members ordered as HallOfFame.keys: (fitness ascending, insertion order
+  // ascending); items order is the reverse.  seq: later insertions compare
+  // greater.  The worst member is the top of a min-heap (no per-node
+  // allocation), member hashes live in a flat open-addressing count table,
+  // and the items order is one sort at the end.
   struct Member {
     double fit;
     long seq;
     int src;
     uint64_t hash;
-    bool operator<(const Member &o) const { return fit < o.fit || (fit == o.fit && seq < o.seq); }
   };
-  std::set<Member> hof;
-  std::unordered_map<uint64_t, int> hashes;  // hash -> members holding it
+  auto worse = [](const Member &x, const Member &y) {  // heap "less": the worst rises to the top
+    return x.fit > y.fit || (x.fit == y.fit && x.seq > y.seq);
+  };
+  std::vector<Member> heap;
+  heap.reserve((size_t)a->maxsize + 1);
+  size_t cap = 64;
+  while (cap < 2 * ((size_t)a->hof_n + (size_t)a->pop_n) + 16) cap <<= 1;
+  struct Slot {
+    uint64_t key;
+    int32_t count, used;
+  };
+  std::vector<Slot> table(cap, Slot{0, 0, 0});
+  auto slot = [&](uint64_t key) -> Slot & {
+    size_t i = (size_t)(key * 0x9E3779B97F4A7C15ull) & (cap - 1);
+    while (table[i].used && table[i].key != key) i = (i + 1) & (cap - 1);
+    if (!table[i].used) table[i] = Slot{key, 0, 1};
+    return table[i];
+  };
   long seq = 0;
-  // existing members, given best first (items order): insert worst first
+  // existing members, given best first (items order): the worst gets the oldest seq
   for (int j = a->hof_n - 1; j >= 0; --j) {
-    hof.insert({a->hof_fitness[j], seq++, j, a->hof_hash[j]});
-    hashes[a->hof_hash[j]] += 1;
+    heap.push_back({a->hof_fitness[j], seq++, j, a->hof_hash[j]});
+    slot(a->hof_hash[j]).count += 1;
   }
+  std::make_heap(heap.begin(), heap.end(), worse);
   auto insert = [&](int i) {
-    hof.insert({a->pop_fitness[i], seq++, a->hof_n + i, a->pop_hash[i]});
-    hashes[a->pop_hash[i]] += 1;
+    heap.push_back({a->pop_fitness[i], seq++, a->hof_n + i, a->pop_hash[i]});
+    std::push_heap(heap.begin(), heap.end(), worse);
+    slot(a->pop_hash[i]).count += 1;
   };
   for (int i = 0; i < a->pop_n; ++i) {
-    if (hof.empty() && a->maxsize != 0) {  // DEAP: an empty hall takes population[0]
+    if (heap.empty() && a->maxsize != 0) {  // DEAP: an empty hall takes population[0]
       insert(0);
       continue;
     }
     if (a->maxsize == 0) continue;
     const double f = a->pop_fitness[i];
-    const bool better = f > hof.begin()->fit;  // ind.fitness > self[-1].fitness
-    if (!(better || (int)hof.size() < a->maxsize)) continue;
-    if (hashes.count(a->pop_hash[i]) && hashes[a->pop_hash[i]] > 0) continue;  // similar to a member
-    if ((int)hof.size() >= a->maxsize) {  // remove(-1): the worst, oldest among equal keys
-      auto worst = hof.begin();
-      hashes[worst->hash] -= 1;
-      hof.erase(worst);
+    const bool better = f > heap.front().fit;  // ind.fitness > self[-1].fitness
+    if (!(better || (int)heap.size() < a->maxsize)) continue;
+    if (slot(a->pop_hash[i]).count > 0) continue;  // similar to a member
+    if ((int)heap.size() >= a->maxsize) {  // remove(-1): the worst, oldest among equal keys
+      std::pop_heap(heap.begin(), heap.end(), worse);
+      slot(heap.back().hash).count -= 1;
+      heap.pop_back();
     }
     insert(i);
   }
-  int j = 0;
-  for (auto it = hof.rbegin(); it != hof.rend(); ++it, ++j) {
-    a->new_src[j] = it->src;
-    a->new_fitness[j] = it->fit;
+  // items order: best first, newest first among equal fitness
+  std::sort(heap.begin(), heap.end(), worse);
+  for (size_t j = 0; j < heap.size(); ++j) {
+    a->new_src[j] = heap[j].src;
+    a->new_fitness[j] = heap[j].fit;
   }
-  *a->new_n = j;
+  *a->new_n = (int32_t)heap.size();
   return PG_OK;
 }
 

@@ -81,6 +81,7 @@ class DeviceGA:
         self.logbook = []
         self.last = None       # EvalResult of the latest evaluation (this rank's rows)
         self.eval_events = None  # optional (start, end) HIP events recorded around the evaluation launch
+        self.profile = None      # dict: when set, step() adds per-phase wall ms (with device syncs)
 
     # ------------------------------------------------------------ views
     @property
@@ -234,20 +235,36 @@ class DeviceGA:
             self.generation = 0
             return self._record(0, nevals)
         g = self.generation + 1
+        self._mark(None)
         chosen = D.select_tournament_ranked(self.fitness, self.P, self.tournsize, seed=self.seed, generation=g)
         off = self.spare[self.H:]
         _, invalid = D.vary(self.population, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu,
                             self.sigma, self.indpb, seed=self.seed, generation=g, out=off)
         inv = invalid.bool()
         inherited = self.fitness[chosen.long()]  # a clone keeps its parent's fitness (varAnd)
+        self._mark("select_vary")
         fit = self._evaluate(g, off)
         new_fit = torch.where(inv, fit, inherited)
+        self._mark("evaluate")
         self._check(new_fit)
         self._hof_update(new_fit, off, self.spare)
+        self._mark("hall_of_fame")
         self.fitness = new_fit
         self.store, self.spare = self.spare, self.store
         self.generation = g
-        return self._record(g, int(inv.sum()))
+        rec = self._record(g, int(inv.sum()))
+        self._mark("record")
+        return rec
+
+    def _mark(self, phase):
+        if self.profile is None:
+            return
+        import time
+        torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        if phase is not None:
+            self.profile[phase] = self.profile.get(phase, 0.0) + (now - self._t_mark) * 1e3
+        self._t_mark = now
 
     def run(self, ngen: int, verbose: bool = False) -> list:
         """algorithms.eaSimple(..., ngen): the initial evaluation if pending, then ngen generations."""
