@@ -35,6 +35,10 @@
  * pg_row_hash                    DEAP HallOfFame's similar (operator.eq on the
  *                                gene lists, ga.py:78) as a 64-bit row hash
  * pg_hof_update (host)           tools.HallOfFame.update (eaSimple, main.py:165-170)
+ * pg_render_frames               the frame env.step returns (main.py:77; the build's
+ *                                rasteriser of its SoA state in config.py colours)
+ * pg_find_stuff                  find_stuff utils.py:14-19 / get_rect_quickly
+ *                                utils.py:60-68, batched
  */
 #ifndef PONG_GA_H
 #define PONG_GA_H
@@ -256,6 +260,13 @@ int32_t pg_row_hash(const void *rows, int64_t stride, const int32_t *index, int3
                     int32_t dtype, uint64_t *hash, void *stream);
 /* Host only (no device memory, no GPU needed). */
 int32_t pg_hof_update(const pg_hof_args *args);
+/* frames [n, 210, 160, 3] uint8 (16-byte aligned) from the SoA state [PG_STATE_FIELDS, n]:
+ * background, the walls above/below the playfield, both paddles, the ball if visible. */
+int32_t pg_render_frames(const int32_t *state, int32_t n, uint8_t *frames, void *stream);
+/* out [n, 3, 2] f64: find_stuff's (row, col) centroids of the ball, left and right
+ * colours in the crop rows 34..193, matched per channel as get_rect_quickly does;
+ * NaN for None.  frame_stride in bytes (>= 100800, multiple of 16). */
+int32_t pg_find_stuff(const uint8_t *frames, int64_t frame_stride, int32_t n, double *out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -335,3 +335,33 @@ def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash):
                     ph.ctypes.data, ctypes.addressof(new_n), src.ctypes.data, fit.ctypes.data)
     L.check("pg_hof_update", L.lib().pg_hof_update(ctypes.byref(a)))
     return src[: new_n.value].copy(), fit[: new_n.value].copy()
+
+
+FRAME_SHAPE = (210, 160, 3)  # obs.npy
+
+
+def render_frames(state: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
+    """pg_render_frames: [n, 210, 160, 3] uint8 frames of the SoA game states."""
+    n = state.shape[1] if n is None else int(n)
+    _need(state, "state", torch.int32, state.device, (L.PG_STATE_FIELDS, n))
+    frames = torch.empty((n,) + FRAME_SHAPE, dtype=torch.uint8, device=state.device)
+    with torch.cuda.device(state.device):
+        L.check("pg_render_frames", L.lib().pg_render_frames(_ptr(state), n, _ptr(frames), _stream(state.device)))
+    return frames
+
+
+def find_stuff(frames: torch.Tensor) -> torch.Tensor:
+    """pg_find_stuff: [n, 3, 2] f64 centroids (ball, left, right) of [n, 210, 160, 3]
+    uint8 frames, NaN where find_stuff returns None."""
+    if frames.dim() == 3:
+        frames = frames[None]
+    if frames.dtype != torch.uint8 or tuple(frames.shape[1:]) != FRAME_SHAPE or not frames.is_contiguous():
+        raise ValueError("frames must be contiguous uint8 [n, 210, 160, 3]")
+    if frames.data_ptr() % 16:
+        frames = frames.clone()
+    n = frames.shape[0]
+    out = torch.empty((n, 3, 2), dtype=torch.float64, device=frames.device)
+    with torch.cuda.device(frames.device):
+        L.check("pg_find_stuff", L.lib().pg_find_stuff(_ptr(frames), frames[0].numel() if n else 100800, n, _ptr(out),
+                                                       _stream(frames.device)))
+    return out

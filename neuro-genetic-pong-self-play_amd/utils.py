@@ -19,6 +19,26 @@ from config import GAME_PLAYABLE_HEIGHT, GAME_WIDTH, SCALED_PADDLE_HEIGHT, TIME_
 from numpy_nn import NeuralNetwork
 
 
+def find_stuff(observation):
+    """find_stuff (utils.py:14-19): the (row, col) centroids of the ball, left and
+    right paddle colours in a 210x160x3 frame, each None when absent -- computed
+    by pg_find_stuff on the device (per-channel matching as get_rect_quickly,
+    utils.py:60-68).  Returns a [3, 2] float array when all three are present,
+    else numpy < 1.24's object array of three entries."""
+    import torch
+    from pong_amd import device as _device
+    dev = torch.device(DEVICE)  # noqa: F405
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    frame = torch.as_tensor(np.ascontiguousarray(observation, dtype=np.uint8), device=dev)
+    got = _device.find_stuff(frame)[0].cpu().numpy()
+    if not np.isnan(got).any():
+        return got
+    out = np.empty(3, dtype=object)
+    out[:] = [None if np.isnan(v).any() else v for v in got]
+    return out
+
+
 def keep_within_game_bounds_please(paddle, action):
     """Force a paddle whose centroid row is within 16 px of a wall back toward
     the middle (utils.py:71-77); ``paddle`` is a (row, col) centroid or None."""

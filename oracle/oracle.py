@@ -79,6 +79,9 @@ def lib() -> ctypes.CDLL:
         L.or_eval_population.argtypes = [
             ctypes.c_int, ctypes.c_int, dp, ctypes.c_int64, dp, ctypes.c_int64, ip, ip, dp,
             ctypes.POINTER(OrNet), ctypes.c_uint64, dp, dp, ip, ip, dp, ip, ctypes.c_int]
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.or_render.argtypes = [ctypes.POINTER(OrState), u8p]
+        L.or_find_stuff.argtypes = [u8p, dp]
         _lib = L
     return _lib
 
@@ -187,3 +190,22 @@ def eval_population(genomes, nodes, kind, opp_index, mult, opponents=None, bias=
         _dp(total), _ip(status), int(n_threads))
     return {"fitness": fitness, "rewards": rewards, "scores": scores, "frames": frames,
             "total_frames": total, "status": status, "first_error": first_err}
+
+
+# ------------------------------------------------------------- pixel path
+def render(state: dict) -> np.ndarray:
+    """or_render: the [210, 160, 3] uint8 frame of a state (Env.snapshot() keys)."""
+    s = OrState(**{k: int(state[k]) for k in ("ball_x", "ball_y", "ball_visible", "lpy", "rpy")})
+    frame = np.zeros((210, 160, 3), dtype=np.uint8)
+    lib().or_render(ctypes.byref(s), frame.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return frame
+
+
+def find_stuff(frame: np.ndarray) -> np.ndarray:
+    """or_find_stuff: [3, 2] f64 centroids (ball, left, right), NaN for None."""
+    f = np.ascontiguousarray(frame, dtype=np.uint8)
+    if f.shape != (210, 160, 3):
+        raise ValueError("frame must be [210, 160, 3] uint8")
+    out = np.zeros(6, dtype=np.float64)
+    lib().or_find_stuff(f.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _dp(out))
+    return out.reshape(3, 2)

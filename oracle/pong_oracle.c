@@ -334,3 +334,47 @@ int or_eval_population(int n, int n_games, const double *genomes, int64_t stride
   }
   return first_err;
 }
+
+/* ------------------------------------------------------------ pixel path -- */
+static const uint8_t OR_COLOURS[4][3] = {{144, 72, 17},    /* BG_COLOUR        config.py */
+                                        {236, 236, 236},  /* BALL_COLOUR                */
+                                        {213, 130, 74},   /* LEFT_GUY_COLOUR            */
+                                        {92, 186, 92}};   /* RIGHT_GUY_COLOUR           */
+
+static void paint(uint8_t *frame, int r0, int r1, int c0, int c1, int colour) { /* rows [r0,r1), cols [c0,c1) */
+  for (int r = r0; r < r1; ++r)
+    for (int c = c0; c < c1; ++c)
+      for (int ch = 0; ch < 3; ++ch) frame[(r * 160 + c) * 3 + ch] = OR_COLOURS[colour][ch];
+}
+
+void or_render(const or_pong_state *s, uint8_t *frame) {
+  const int top = 34; /* GAME_TOP */
+  paint(frame, 0, 210, 0, 160, 0);
+  paint(frame, 24, 34, 0, 160, 1);
+  paint(frame, 194, 210, 0, 160, 1);
+  const int pys[2] = {s->lpy, s->rpy}, xs[2] = {OR_LEFT_PADDLE_X, OR_RIGHT_PADDLE_X};
+  for (int k = 0; k < 2; ++k) {
+    const int lo = pys[k] < 0 ? 0 : pys[k];
+    const int hi = pys[k] + OR_PADDLE_H - 1 > OR_FIELD_H - 1 ? OR_FIELD_H - 1 : pys[k] + OR_PADDLE_H - 1;
+    paint(frame, top + lo, top + hi + 1, xs[k], xs[k] + OR_PADDLE_W, 2 + k);
+  }
+  if (s->ball_visible) paint(frame, top + s->ball_y, top + s->ball_y + OR_BALL_H, s->ball_x, s->ball_x + OR_BALL_W, 1);
+}
+
+void or_find_stuff(const uint8_t *frame, double *out) {
+  /* np.average(np.argwhere(crop == colour)[:, :-1], axis=0): one (row, col)
+   * per matching CHANNEL; integer sums are exact, one rounding in the mean */
+  for (int k = 0; k < 3; ++k) {
+    long long n = 0, rs = 0, cs = 0;
+    for (int r = 0; r < 160; ++r)
+      for (int c = 0; c < 160; ++c)
+        for (int ch = 0; ch < 3; ++ch)
+          if (frame[((34 + r) * 160 + c) * 3 + ch] == OR_COLOURS[k + 1][ch]) {
+            n += 1;
+            rs += r;
+            cs += c;
+          }
+    out[2 * k] = n ? (double)rs / (double)n : NAN;
+    out[2 * k + 1] = n ? (double)cs / (double)n : NAN;
+  }
+}

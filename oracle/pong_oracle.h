@@ -117,6 +117,15 @@ int or_eval_population(int n, int n_games, const double *genomes, int64_t stride
                        int32_t *frames, double *total_frames, int32_t *status,
                        int n_threads);
 
+/* ---- pixel path (utils.py:14-19, 60-68; the build's frame of its state) ---- */
+#define OR_FRAME_BYTES (210 * 160 * 3)
+/* The 210x160x3 frame of a state in config.py colours: background, walls at
+ * rows 24..33 and 194..209, both paddles clipped to the playfield, the ball. */
+void or_render(const or_pong_state *s, uint8_t *frame);
+/* find_stuff: out[0..5] = ball, left, right (row, col) centroids over the crop
+ * rows 34..193, matched per channel (get_rect_quickly); NaN for None. */
+void or_find_stuff(const uint8_t *frame, double *out);
+
 #ifdef __cplusplus
 }
 #endif

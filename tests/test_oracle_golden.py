@@ -146,3 +146,27 @@ def test_oracle_physics_invariants(oracle):
             if env.done():  # 21 points: no further serve (the emulator's episode end)
                 assert max(s["score1"], s["score2"]) == 21
                 break
+
+
+def test_oracle_find_stuff_on_reference_fixture(oracle, golden):
+    """find_stuff on the reference's own obs.npy (tests.py:48-57; copied as a
+    data fixture) and on a zero frame, against the real reference's outputs."""
+    h = golden("helpers.json")
+    obs = golden("obs.npy")
+    np.testing.assert_array_equal(oracle.find_stuff(obs), np.array(h["find_stuff_obs"]))
+    assert h["find_stuff_zero"] == [None, None, None]
+    assert np.isnan(oracle.find_stuff(np.zeros_like(obs))).all()
+
+
+def test_oracle_render_then_find_stuff_matches_reference(oracle, golden):
+    """The reference's find_stuff on 300 rendered states (tests/golden/centroids.npy)
+    equals the oracle's render + find_stuff restatement."""
+    c = golden("centroids.npy")
+    for row in c:
+        lpy, rpy, vis, by, bx = (int(v) for v in row[:5])
+        st = {"lpy": lpy, "rpy": rpy, "ball_visible": vis, "ball_y": by, "ball_x": bx}
+        got = oracle.find_stuff(oracle.render(st))
+        want = row[5:].reshape(3, 2).copy()
+        if not vis:
+            want[0] = np.nan
+        np.testing.assert_array_equal(got, want)
