@@ -68,3 +68,5 @@ PRECISION = "certified"
 GENOME_DTYPE = "float64"
 # "cuda" = the process's current HIP device (one process per GPU).
 DEVICE = "cuda"
+# evaluate(render=True) writes each replayed game here as game_<g>.gif (no viewer window).
+REPLAY_DIR = "replays"

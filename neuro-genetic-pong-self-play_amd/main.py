@@ -60,10 +60,32 @@ def evaluate_population(individuals):
 
 
 def evaluate(individual=None, render=RENDER):  # noqa: F405
-    """Average reward of the individual's GAMES_TO_PLAY games (main.py:28-66)."""
+    """Average reward of the individual's GAMES_TO_PLAY games (main.py:28-66).
+
+    ``render=True`` (render_game, main.py:115-125) writes each game as an
+    animated GIF under REPLAY_DIR instead of a gym viewer window: the games are
+    replayed from their action traces and rasterised on the device
+    (pong_amd.replay)."""
     if render:
-        raise NotImplementedError("rendering (main.py:115-125) is outside the MI355X hot path")
+        return _evaluate_rendered(individual)
     return next(evaluate_population([individual]))
+
+
+def _evaluate_rendered(individual):
+    import os
+
+    from pong_amd import replay
+    ev = _evaluator()
+    genes = utils.calculate_gene_size()
+    kind, opp, mult, members = schedule.reference_schedule(1, GAMES_TO_PLAY, hall_of_fame,  # noqa: F405
+                                                           pick_hall_of_famer)
+    genomes = runtime.genomes_to_device([individual], genes, ev)
+    opponents = runtime.genomes_to_device(members, genes, ev) if members else None
+    res, frames = replay.replay(ev, genomes[0], kind[0], opp[0], mult[0], opponents=opponents)
+    for g, f in enumerate(frames):
+        if len(f):
+            replay.write_gif(f, os.path.join(REPLAY_DIR, f"game_{g}.gif"), fps=FPS)  # noqa: F405
+    return next(_fitness_tuples(res.fitness.cpu().numpy(), res.status.cpu().numpy()))
 
 
 evaluate.__pong_batch__ = evaluate_population

@@ -30,15 +30,22 @@ def gather_fitness(local: torch.Tensor, n_total: int, group=None) -> torch.Tenso
     if local.shape[0] != hi - lo:
         raise ValueError(f"rank {rank} holds {local.shape[0]} fitness values, expected {hi - lo}")
     width = -(-n_total // world)  # ceil: all_gather needs equal sizes
-    buf = torch.zeros(width, dtype=local.dtype, device=local.device)
-    buf[: hi - lo] = local
-    out = torch.empty(width * world, dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, buf, group=group)
+    # gloo (the CPU test backend, also used for several ranks on one GPU) moves
+    # host tensors; RCCL ("nccl") gathers device memory over xGMI directly
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if stage else local.device
+    buf = torch.zeros(width, dtype=local.dtype, device=dev)
+    buf[: hi - lo] = local.to(dev)
+    out = torch.empty(width * world, dtype=local.dtype, device=dev)
+    if stage:
+        dist.all_gather(list(out.split(width)), buf, group=group)
+    else:
+        dist.all_gather_into_tensor(out, buf, group=group)
     parts = []
     for r in range(world):
         a, b = shard_range(n_total, r, world)
         parts.append(out[r * width: r * width + (b - a)])
-    return torch.cat(parts)
+    return torch.cat(parts).to(local.device)
 
 
 def evaluate_sharded(evaluate_rows, n_total: int, group=None):

@@ -159,3 +159,11 @@ def test_schedule_semantics():
             assert m[r, g] == shadow[0].fitness.values[0]
     assert [id(x) for x in hof.items] == [id(x) for x in shadow]  # shuffled in place
     assert np.all(k[:, 3:] == 3) and np.all(m[:, :3] == 1)
+
+
+def test_replay_game_seed_matches_oracle(oracle):
+    """pong_amd.replay's host game seeds equal the physics' (or_game_seed = pg_device game_seed)."""
+    from pong_amd.replay import game_seed
+    for base in (0, 1, 12345, 2**63 + 7, 2**64 - 1):
+        for g in range(8):
+            assert game_seed(base, g) == oracle.lib().or_game_seed(base, g)
