@@ -124,6 +124,7 @@ def main():
     slow_local = 0
     cert_local = [0, 0, 0]  # certificate failures, decided by the service wave, decided in-wave
     passes_local = 0        # k_wide: network weight passes (each streams one network's genes once)
+    skip_local = 0          # episode frames of periodic rallies not simulated (counters[8])
     kernel_ms = []
     counters = []
     ga.eval_events = (ev_start, ev_end)
@@ -147,9 +148,11 @@ def main():
         for i in range(3):
             cert_local[i] += int(c[4 + i])
         passes_local += int(c[7])
+        skip_local += int(c[8])
 
     t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)]
-                     + [float(v) for v in cert_local] + [float(passes_local)], dtype=torch.float64, device=dev)
+                     + [float(v) for v in cert_local] + [float(passes_local), float(skip_local)],
+                     dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
@@ -160,15 +163,17 @@ def main():
         kernel_ms_mean = float(tsum[4]) / world / args.steps
         cert_all = [float(v) for v in tsum[5:8]]
         passes_all = float(tsum[8])
+        skip_all = float(tsum[9])
     else:
         steps_all, fwd_all, slow_all = float(t[1]), float(t[2]), float(t[3])
         kernel_ms_mean = float(t[4]) / args.steps
         cert_all = [float(v) for v in t[5:8]]
         passes_all = float(t[8])
+        skip_all = float(t[9])
 
     if rank == 0 and args.config == "wide":
         out = wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all,
-                          passes_all, kernel_ms_mean)
+                          passes_all, kernel_ms_mean, skip_all)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, shape, ga, chunk=8,
                                               max_rows=256)
@@ -202,6 +207,8 @@ def main():
                        "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                        "parallelism": f"dp{world}" if world > 1 else "dp1",
                        "env_steps_per_generation": steps_all / args.steps,
+                       "periodic_rally_frames_skipped_per_generation": skip_all / args.steps,
+                       "episode_frames_per_sec_incl_skipped": (steps_all + skip_all) / elapsed,
                        "certificate_failures_per_forward": cert_all[0] / max(fwd_all, 1.0),
                        "failures_decided_in_wave": cert_all[2] / max(cert_all[0], 1.0),
                        "failures_decided_by_service_f64_certificate": cert_all[1] / max(cert_all[0], 1.0),
@@ -231,7 +238,7 @@ def main():
 
 
 def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all, passes_all,
-                kernel_ms_mean):
+                kernel_ms_mean, skip_all=0.0):
     """BASELINE config 5: the generation step with the wide MLP; k_wide is
     HBM-bound (its W2 stream), so the roofline is bytes of weights streamed
     per launch over the launch time against the 8 TB/s HBM peak."""
@@ -262,6 +269,7 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
                    "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                    "parallelism": f"dp{world}" if world > 1 else "dp1",
                    "env_steps_per_generation": steps_all / args.steps,
+                   "periodic_rally_frames_skipped_per_generation": skip_all / args.steps,
                    "network_passes_per_generation": passes_all / args.steps,
                    "forwards_per_network_pass": fwd_all / max(passes_all, 1.0)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

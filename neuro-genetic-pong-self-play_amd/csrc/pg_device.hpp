@@ -130,6 +130,45 @@ struct Pong {
   }
 };
 
+// ---- periodic rallies (DESIGN.md "Periodic rallies") ----
+// Everything that decides the rest of an episode while no point is scored:
+// the Pong state after a frame's step and the two actions decided in that
+// frame (the next frame's "last ball" is this state's ball).  hits only acts
+// through min(2 + hits/4, 4), so it is capped at 8; the scores, seed and
+// player mode are constant between points.  61 bits; injective on reachable
+// states (bx < 160, by < 157, |vx| <= 4, |vy| <= 3, timer <= 30, point <= 42,
+// paddle top in [-8, 152]).  Two equal keys at two frames of one point mean
+// the rally is periodic: no point is ever scored again, and the game ends at
+// the frame where the no-score counter passes TIMEOUT_THRESH (main.py:102-107).
+__device__ inline uint64_t rally_key(const Pong &s, int act_r, int act_l) {
+  uint64_t k = (uint64_t)(s.bx & 255);
+  k = (k << 8) | (uint64_t)(s.by & 255);
+  k = (k << 4) | (uint64_t)(s.vx & 15);
+  k = (k << 4) | (uint64_t)(s.vy & 15);
+  k = (k << 1) | (uint64_t)(s.vis & 1);
+  k = (k << 5) | (uint64_t)(s.timer & 31);
+  k = (k << 1) | (uint64_t)(s.dir > 0);
+  k = (k << 4) | (uint64_t)(s.hits < 8 ? s.hits : 8);
+  k = (k << 6) | (uint64_t)(s.point & 63);
+  k = (k << 8) | (uint64_t)((s.lpy + 8) & 255);
+  k = (k << 8) | (uint64_t)((s.rpy + 8) & 255);
+  k = (k << 2) | (uint64_t)(act_r & 3);
+  k = (k << 2) | (uint64_t)(act_l & 3);
+  return k;
+}
+// Brent's cycle search over one point: the key is saved when the no-score
+// counter reaches kRallyStart and re-saved each time the distance doubles;
+// keys are compared every kRallyStride frames (a multiple of the period is
+// then still met within kRallyStride periods).
+#ifndef PG_RALLY_START
+#define PG_RALLY_START 256
+#endif
+#ifndef PG_RALLY_STRIDE
+#define PG_RALLY_STRIDE 4
+#endif
+constexpr int kRallyStart = PG_RALLY_START;
+constexpr int kRallyStride = PG_RALLY_STRIDE;
+
 // Doubled centroid row of a paddle clipped to rows [0,160): what
 // get_rect_quickly (utils.py:60-68) returns for the rendered rectangle, x2.
 __device__ inline int paddle_c2(int py) {

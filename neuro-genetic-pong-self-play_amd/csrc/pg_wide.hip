@@ -39,8 +39,9 @@ constexpr int kTileRowBytes = 128, kTilePitch = 144;
 constexpr int kDepth = PG_WIDE_DEPTH;  // register sets in the W2 tile ring (2 and 3 measured equal)
 
 // LDS carve (bytes): feats [NC][8] f64 | outputs [NC][4] f64 | control |
-// h1 [C2][NC] f64 | tile [512][144 B], reused for h2 [C3][NC] f64 after layer 2.
-constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffH1 = 2048;
+// opponent rows | rally keys | h1 [C2][NC] f64 | tile [512][144 B], reused for
+// h2 [C3][NC] f64 after layer 2.
+constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffRally = 2048, kOffH1 = 2304;
 __host__ __device__ constexpr int align16(int v) { return (v + 15) & ~15; }
 
 __host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b) {
@@ -104,6 +105,8 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   double *outv = (double *)(lds_raw + kOffOut);  // [NC][4]
   int *ctl = (int *)(lds_raw + kOffCtl);         // [0] genome; frame-parity halves at [8..] and [40..]
   long long *orow = (long long *)(lds_raw + kOffOrow);  // [NG] opponent row offsets (elements)
+  uint64_t *rkey = (uint64_t *)(lds_raw + kOffRally);    // [NG] Brent's saved rally key per game
+  int *rat = (int *)(lds_raw + kOffRally + 64), *rspan = (int *)(lds_raw + kOffRally + 96);
   double *h1 = (double *)(lds_raw + kOffH1);            // [C2][NC]
   unsigned char *tile = lds_raw + kOffH1 + align16(C2 * NC * 8);
   double *h2 = (double *)tile;  // [C3][NC], after layer 2
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
   const int n_games = p.n_games;
-  uint64_t c_steps = 0, c_fwd = 0, c_games = 0, c_streams = 0;
+  uint64_t c_steps = 0, c_fwd = 0, c_games = 0, c_streams = 0, c_skip = 0;
 
   for (;;) {  // genomes, one per workgroup at a time
     if (t == 0) ctl[0] = (int)atomicAdd(p.work, 1u);
@@ -401,6 +404,27 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             timeout = 0;
           }
         }
+#ifndef PG_NO_RALLY_SKIP
+        // a periodic rally ends at the timeout with nothing else changed (pg_device.hpp rally_key)
+        if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
+        !p.trace) {
+          const uint64_t key = rally_key(st, act_r, act_l);
+          if (timeout == kRallyStart) {
+            rkey[lane] = key;
+            rat[lane] = timeout;
+            rspan[lane] = kRallyStart;
+          } else if (rkey[lane] == key) {
+            const int rest = kTimeoutThresh + 1 - timeout;
+            frames += rest;
+            c_skip += rest;
+            timeout = kTimeoutThresh + 1;
+          } else if (timeout - rat[lane] == rspan[lane]) {
+            rkey[lane] = key;
+            rat[lane] = timeout;
+            rspan[lane] *= 2;
+          }
+        }
+#endif
         if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
           finish_game(p, w, st, frames, total);
           active = false;
@@ -411,7 +435,8 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
     }
   }
   if (p.counters && wid == 0 && c_games) {
-    atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)c_steps);
+    atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)(c_steps - c_skip));
+    if (c_skip) atomicAdd((unsigned long long *)&p.counters[8], (unsigned long long)c_skip);
     atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
     atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
   }

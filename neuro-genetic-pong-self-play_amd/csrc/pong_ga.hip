@@ -693,6 +693,8 @@ struct SlowSlot {
   volatile int n_memo;  // decisions memoised for the current game's network
   volatile uint64_t memo_key[kMemo];
   volatile int memo_idx[kMemo];
+  uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
+  int rally_at, rally_span;
 };
 
 // The plateau certificate in f32, tried by the game wave itself where
@@ -1000,7 +1002,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   Pong st;
   int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
   const WT *gm = genomes;
-  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0;
+  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0;
 
   int w;
   {
@@ -1121,6 +1123,33 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         timeout = 0;
       }
     }
+#ifndef PG_NO_RALLY_SKIP
+    // a periodic rally ends at the timeout with nothing else changed: jump there
+    // (never while tracing, which records every frame's actions)
+    if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
+        !p.trace) {
+      const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
+      const uint64_t key = rally_key(st, act_r, act_l);
+      if (timeout == kRallyStart) {
+        if (lig == 0) {
+          slots[rs].rally_key = key;
+          slots[rs].rally_at = timeout;
+          slots[rs].rally_span = kRallyStart;
+        }
+      } else if (slots[rs].rally_key == key) {
+        const int rest = kTimeoutThresh + 1 - timeout;
+        frames += rest;
+        skipped += rest;
+        timeout = kTimeoutThresh + 1;
+      } else if (timeout - slots[rs].rally_at == slots[rs].rally_span) {
+        if (lig == 0) {
+          slots[rs].rally_key = key;
+          slots[rs].rally_at = timeout;
+          slots[rs].rally_span = 2 * slots[rs].rally_span;
+        }
+      }
+    }
+#endif
     if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
       if (lig == 0) finish_game(p, w, st, frames, total);
 #ifdef PG_TIMELINE
@@ -1142,9 +1171,11 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   }
   if (p.counters && c_games) {
     if (lig == 0) {
-      atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)c_steps);
+      // env steps simulated: the episodes' frames minus those a periodic rally skipped
+      atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)(c_steps - skipped));
       atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
       atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
+      if (skipped) atomicAdd((unsigned long long *)&p.counters[8], (unsigned long long)skipped);
     }
     if (hl == 0 && slow) atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
     if (hl == 0 && fails) atomicAdd((unsigned long long *)&p.counters[4], (unsigned long long)fails);

@@ -55,9 +55,10 @@ class EvalResult:
     frames: torch.Tensor        # [n, games] int32 env steps
     total_frames: torch.Tensor  # [n, games] f64
     status: torch.Tensor        # [n] int32, 1 = ZeroDivisionError
-    counters: torch.Tensor      # [8] int64: env steps, NN forwards, numpy-order f64 forwards, games,
-    #                             certificate failures, decided by the service's certified f64 rules,
-    #                             decided in-wave by the f32 plateau rule, 0
+    counters: torch.Tensor      # [12] int64 (pg_eval_args.counters): [0] env steps simulated, [1] NN
+    #                             forwards, [2] numpy-order f64 forwards, [3] games, [4..6] certificate
+    #                             cascade (split), [7] network passes (wide), [8] frames of periodic
+    #                             rallies not simulated (the episodes' frames = [0] + [8])
 
 
 class Evaluator:
@@ -139,7 +140,7 @@ class Evaluator:
                 frames=torch.empty((n, games), dtype=torch.int32, device=dev),
                 total_frames=torch.empty((n, games), dtype=torch.float64, device=dev),
                 status=torch.empty(n, dtype=torch.int32, device=dev),
-                counters=torch.zeros(8, dtype=torch.int64, device=dev))
+                counters=torch.zeros(12, dtype=torch.int64, device=dev))
         else:
             out.counters.zero_()
         trace = None

@@ -68,7 +68,7 @@ def test_wide_matches_oracle(gpu, oracle, shape, bias, dt):
     res, _ = _eval(ev, gpu, genomes, opponents, kinds, opp, mult)
     ref = oracle.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents, bias=bias, n_threads=8)
     _same(res, ref)
-    assert int(res.counters[0]) == int(ref["frames"].sum())
+    assert int(res.counters[0]) + int(res.counters[8]) == int(ref["frames"].sum())
     assert int(res.counters[3]) == n * 6
 
 
@@ -90,7 +90,7 @@ def test_wide_equals_general_with_traces(gpu, n_games):
                    trace_cap=cap)
     _same(rw, rg)
     assert torch.equal(tw, tg)
-    assert torch.equal(rw.counters[:4], rg.counters[:4])
+    assert torch.equal(rw.counters[1:4], rg.counters[1:4]) and int(rw.counters[8]) == 0  # tracing: no skips
 
 
 def test_wide_config5_shape_matches_oracle(gpu, oracle):
@@ -131,4 +131,10 @@ def test_wide_selfplay_properties(gpu):
     r2, _ = ev.evaluate(genomes[perm].contiguous(), kind[perm].contiguous(), opp[perm].contiguous(),
                         mult[perm].contiguous(), opponents=opponents)
     assert torch.equal(r2.fitness, f1[perm]) and torch.equal(r2.frames, r1.frames[perm])
-    assert int(r1.counters[3]) == n * 6 and int(r1.counters[0]) == int(r1.frames.sum())
+    assert int(r1.counters[3]) == n * 6 and int(r1.counters[0]) + int(r1.counters[8]) == int(r1.frames.sum())
+    # the periodic-rally jump changes nothing: the general kernel simulates every frame
+    sel = torch.arange(0, n, 13, device=gpu)
+    rg, _ = ev.evaluate(genomes[sel].contiguous(), kind[sel].contiguous(), opp[sel].contiguous(),
+                        mult[sel].contiguous(), opponents=opponents, kernel="general")
+    assert torch.equal(rg.fitness, r1.fitness[sel]) and torch.equal(rg.frames, r1.frames[sel])
+    assert torch.equal(rg.scores, r1.scores[sel]) and torch.equal(rg.total_frames, r1.total_frames[sel])
