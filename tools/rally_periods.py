@@ -1,3 +1,11 @@
+#!/usr/bin/env python3
+"""Analysis (CPU, the oracle as the simulator): how long after the last point
+do timeout games become periodic, and with what period?  Plays 1 500
+self-play games of the bench distribution ([6,64,3], N(0,3) genes) with
+traces, re-steps the timeout games and finds the first repeat of the full
+rally state (pg_device.hpp rally_key's fields).  Measured: 55 timeouts, all
+periodic with period 60, first repeat ~460 frames after the last point.
+usage: python tools/rally_periods.py   (from the repository root)"""
 import sys, numpy as np
 sys.path.insert(0, 'oracle'); import oracle as O
 rng = np.random.default_rng(0)
