@@ -216,10 +216,14 @@ typedef struct pg_schedule_args {
 
 /* HallOfFame.update (DEAP) over host arrays.  Members are in HallOfFame.items
  * order (best first; among equal fitness the newest first); "similar" is the
- * equality of pg_row_hash values.  Sequential semantics: an individual enters
+ * equality of pg_row_hash values (or of any other class labels: when every
+ * label lies in [0, hof_n + pop_n), e.g. dense ids from a device-side unique,
+ * counts are kept in a direct-indexed array).  Sequential semantics: an individual enters
  * iff the hall is not full or its fitness beats the worst member strictly,
  * and no member is similar; a full hall drops its last (worst, oldest among
- * equals) member; an empty hall first takes population[0]. */
+ * equals) member; an empty hall first takes population[0].  Fitness must not
+ * be NaN.  O(hof_n + pop_n) given the ranks: while the hall is full its worst
+ * member only moves up the (fitness, age) order. */
 typedef struct pg_hof_args {
   int32_t maxsize;               /* HALL_OF_FAME_AMOUNT (config.py:50) */
   int32_t hof_n;                 /* current members */
@@ -228,6 +232,10 @@ typedef struct pg_hof_args {
   int32_t pop_n;
   const double *pop_fitness;     /* [pop_n] host, population order */
   const uint64_t *pop_hash;      /* [pop_n] host */
+  const int32_t *rank;           /* optional [hof_n + pop_n] host: each entry's position in the ascending
+                                    order of (fitness, age) -- old member j is entry j, aged so that
+                                    member hof_n - 1 is the oldest; population row i is entry hof_n + i,
+                                    newer than every member and than rows < i.  NULL: sorted here. */
   int32_t *new_n;                /* out: members after the update */
   int32_t *new_src;              /* out [maxsize]: member j's source: j' < hof_n = old member j',
                                     hof_n + i = population row i */

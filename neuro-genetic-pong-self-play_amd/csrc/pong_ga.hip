@@ -1938,71 +1938,98 @@ int32_t pg_hof_update(const pg_hof_args *a) {
       (a->maxsize > 0 && (!a->new_src || !a->new_fitness)) || (a->hof_n > 0 && (!a->hof_fitness || !a->hof_hash)) ||
       (a->pop_n > 0 && (!a->pop_fitness || !a->pop_hash)))
     return fail(PG_ERR_INVALID, "hof_update: bad sizes or NULL buffers");
-  // Members ordered as HallOfFame.keys: (fitness ascending, insertion order
-  // ascending); items order is the reverse.  seq: later insertions compare
-  // greater.  The worst member is the top of a min-heap (no per-node
-  // allocation), member hashes live in a flat open-addressing count table,
-  // and the items order is one sort at the end.
-  struct Member {
-    double fit;
-    long seq;
-    int src;
-    uint64_t hash;
-  };
-  auto worse = [](const Member &x, const Member &y) {  // heap "less": the worst rises to the top
-    return x.fit > y.fit || (x.fit == y.fit && x.seq > y.seq);
-  };
-  std::vector<Member> heap;
-  heap.reserve((size_t)a->maxsize + 1);
-  size_t cap = 64;
-  while (cap < 2 * ((size_t)a->hof_n + (size_t)a->pop_n) + 16) cap <<= 1;
+  // Entries e < hof_n are the old members (items order), entries hof_n + i the
+  // population.  Rank = position in ascending (fitness, age) order, age as
+  // HallOfFame.keys orders equal fitness: later insertions rank higher.  The
+  // hall is a presence bitmap over ranks; its worst member is the lowest
+  // present rank, which only moves up while the hall is full (an entrant
+  // beats the worst strictly), so each removal is an amortised O(1) scan.
+  const int hn = a->hof_n, pn = a->pop_n, n = hn + pn;
+  auto fit_of = [&](int e) { return e < hn ? a->hof_fitness[e] : a->pop_fitness[e - hn]; };
+  auto hash_of = [&](int e) { return e < hn ? a->hof_hash[e] : a->pop_hash[e - hn]; };
+  auto age_of = [&](int e) { return e < hn ? (hn - 1 - e) : e; };  // old member hn-1 is the oldest
+  std::vector<int32_t> rank_v, by_rank((size_t)n);
+  const int32_t *rank = a->rank;
+  if (!rank) {
+    std::vector<int32_t> order((size_t)n);
+    for (int e = 0; e < n; ++e) order[e] = e;
+    std::sort(order.begin(), order.end(), [&](int x, int y) {
+      const double fx = fit_of(x), fy = fit_of(y);
+      return fx < fy || (fx == fy && age_of(x) < age_of(y));
+    });
+    rank_v.resize((size_t)n);
+    for (int r = 0; r < n; ++r) rank_v[order[r]] = r;
+    rank = rank_v.data();
+  }
+  for (int e = 0; e < n; ++e) {
+    if (rank[e] < 0 || rank[e] >= n) return fail(PG_ERR_INVALID, "hof_update: rank[%d]=%d out of range", e, rank[e]);
+    by_rank[rank[e]] = e;
+  }
+  std::vector<uint64_t> present(((size_t)n + 63) / 64, 0);
+  // Similarity classes: when every hash is a dense class id in [0, n) (DeviceGA
+  // passes torch.unique's inverse), counts are a direct-indexed array; else a
+  // flat open-addressing table keyed by the 64-bit row hash.
+  bool dense = true;
+  for (int e = 0; e < n && dense; ++e) dense = (uint64_t)hash_of(e) < (uint64_t)n;
+  std::vector<int32_t> dense_count(dense ? (size_t)n : 0, 0);
+  size_t cap = 1;
+  if (!dense)
+    while (cap < 2 * (size_t)n + 16) cap <<= 1;
   struct Slot {
     uint64_t key;
     int32_t count, used;
   };
-  std::vector<Slot> table(cap, Slot{0, 0, 0});
-  auto slot = [&](uint64_t key) -> Slot & {
+  std::vector<Slot> table(dense ? 0 : cap, Slot{0, 0, 0});
+  auto count_of = [&](uint64_t key) -> int32_t & {
+    if (dense) return dense_count[key];
     size_t i = (size_t)(key * 0x9E3779B97F4A7C15ull) & (cap - 1);
     while (table[i].used && table[i].key != key) i = (i + 1) & (cap - 1);
     if (!table[i].used) table[i] = Slot{key, 0, 1};
-    return table[i];
+    return table[i].count;
   };
-  long seq = 0;
-  // existing members, given best first (items order): the worst gets the oldest seq
-  for (int j = a->hof_n - 1; j >= 0; --j) {
-    heap.push_back({a->hof_fitness[j], seq++, j, a->hof_hash[j]});
-    slot(a->hof_hash[j]).count += 1;
-  }
-  std::make_heap(heap.begin(), heap.end(), worse);
-  auto insert = [&](int i) {
-    heap.push_back({a->pop_fitness[i], seq++, a->hof_n + i, a->pop_hash[i]});
-    std::push_heap(heap.begin(), heap.end(), worse);
-    slot(a->pop_hash[i]).count += 1;
+  int size = 0, worst = n;  // lowest present rank (n: none)
+  auto add = [&](int e) {
+    const int r = rank[e];
+    present[r >> 6] |= 1ull << (r & 63);
+    count_of(hash_of(e)) += 1;
+    size += 1;
+    worst = r < worst ? r : worst;
   };
-  for (int i = 0; i < a->pop_n; ++i) {
-    if (heap.empty() && a->maxsize != 0) {  // DEAP: an empty hall takes population[0]
-      insert(0);
+  for (int e = 0; e < hn; ++e) add(e);
+  for (int i = 0; i < pn; ++i) {
+    if (size == 0 && a->maxsize != 0) {  // DEAP: an empty hall takes population[0]
+      add(hn);
       continue;
     }
     if (a->maxsize == 0) continue;
     const double f = a->pop_fitness[i];
-    const bool better = f > heap.front().fit;  // ind.fitness > self[-1].fitness
-    if (!(better || (int)heap.size() < a->maxsize)) continue;
-    if (slot(a->pop_hash[i]).count > 0) continue;  // similar to a member
-    if ((int)heap.size() >= a->maxsize) {  // remove(-1): the worst, oldest among equal keys
-      std::pop_heap(heap.begin(), heap.end(), worse);
-      slot(heap.back().hash).count -= 1;
-      heap.pop_back();
+    if (size >= a->maxsize && !(f > fit_of(by_rank[worst]))) continue;  // ind.fitness > self[-1].fitness
+    if (count_of(a->pop_hash[i]) > 0) continue;                        // similar to a member
+    if (size >= a->maxsize) {  // remove(-1): the worst, oldest among equal fitness
+      present[worst >> 6] &= ~(1ull << (worst & 63));
+      count_of(hash_of(by_rank[worst])) -= 1;
+      size -= 1;
+      size_t wd = (size_t)worst >> 6;
+      uint64_t bits = present[wd] & (~0ull << (worst & 63));
+      while (!bits && ++wd < present.size()) bits = present[wd];
+      worst = bits ? (int)(wd * 64 + __builtin_ctzll(bits)) : n;
     }
-    insert(i);
+    add(hn + i);
   }
-  // items order: best first, newest first among equal fitness
-  std::sort(heap.begin(), heap.end(), worse);
-  for (size_t j = 0; j < heap.size(); ++j) {
-    a->new_src[j] = heap[j].src;
-    a->new_fitness[j] = heap[j].fit;
+  // items order: best first, newest first among equal fitness = descending rank
+  int j = 0;
+  for (size_t wd = present.size(); wd-- > 0;) {
+    uint64_t bits = present[wd];
+    while (bits) {
+      const int hi = 63 - __builtin_clzll(bits);
+      bits &= ~(1ull << hi);
+      const int e = by_rank[wd * 64 + hi];
+      a->new_src[j] = e;
+      a->new_fitness[j] = fit_of(e);
+      ++j;
+    }
   }
-  *a->new_n = (int32_t)heap.size();
+  *a->new_n = j;
   return PG_OK;
 }
 

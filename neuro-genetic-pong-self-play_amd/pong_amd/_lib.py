@@ -93,7 +93,7 @@ class PgScheduleArgs(ctypes.Structure):
 class PgHofArgs(ctypes.Structure):
     _fields_ = [
         ("maxsize", ctypes.c_int32), ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("hof_hash", _vp),
-        ("pop_n", ctypes.c_int32), ("pop_fitness", _vp), ("pop_hash", _vp),
+        ("pop_n", ctypes.c_int32), ("pop_fitness", _vp), ("pop_hash", _vp), ("rank", _vp),
         ("new_n", _vp), ("new_src", _vp), ("new_fitness", _vp),
     ]
 

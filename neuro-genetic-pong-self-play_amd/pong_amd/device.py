@@ -316,9 +316,11 @@ def row_hash(rows: torch.Tensor, genes: Optional[int] = None, index: Optional[to
     return out
 
 
-def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash):
+def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash, rank=None):
     """pg_hof_update (host, no GPU): HallOfFame.update over fitness/hash arrays.
 
+    ``rank`` (optional, [len(hof) + len(pop)] int32): the entries' positions in
+    ascending (fitness, age) order (see pg_hof_args.rank); computed here if None.
     Returns (src [new_n] int32, fitness [new_n] f64): member j comes from old
     member src[j] if src[j] < len(hof_fitness), else from population entry
     src[j] - len(hof_fitness)."""
@@ -329,11 +331,17 @@ def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash):
     ph = np.ascontiguousarray(np.asarray(pop_hash, dtype=np.int64)).view(np.uint64)
     if hf.shape != hh.shape or pf.shape != ph.shape:
         raise ValueError("fitness and hash arrays must pair up")
+    rk = None
+    if rank is not None:
+        rk = np.ascontiguousarray(rank, dtype=np.int32)
+        if rk.shape != (hf.shape[0] + pf.shape[0],):
+            raise ValueError("rank must hold one entry per member and population row")
     src = np.zeros(max(maxsize, 1), dtype=np.int32)
     fit = np.zeros(max(maxsize, 1), dtype=np.float64)
     new_n = ctypes.c_int32(0)
     a = L.PgHofArgs(maxsize, hf.shape[0], hf.ctypes.data, hh.ctypes.data, pf.shape[0], pf.ctypes.data,
-                    ph.ctypes.data, ctypes.addressof(new_n), src.ctypes.data, fit.ctypes.data)
+                    ph.ctypes.data, rk.ctypes.data if rk is not None else None, ctypes.addressof(new_n),
+                    src.ctypes.data, fit.ctypes.data)
     L.check("pg_hof_update", L.lib().pg_hof_update(ctypes.byref(a)))
     return src[: new_n.value].copy(), fit[: new_n.value].copy()
 

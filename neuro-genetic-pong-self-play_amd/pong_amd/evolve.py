@@ -76,12 +76,13 @@ class DeviceGA:
         self.hof_fitness = torch.zeros(max(self.H, 1), dtype=torch.float64, device=self.device)
         self.hof_n = 0
         self._hof_fit_host = np.zeros(0, np.float64)   # HallOfFame.items order (best first)
-        self._hof_hash_host = np.zeros(0, np.int64)
+        self.hof_hash = torch.zeros(max(self.H, 1), dtype=torch.int64, device=self.device)  # pg_row_hash
         self.generation = -1  # -1: the initial population is not evaluated yet
         self.logbook = []
         self.last = None       # EvalResult of the latest evaluation (this rank's rows)
         self.eval_events = None  # optional (start, end) HIP events recorded around the evaluation launch
         self.profile = None      # dict: when set, step() adds per-phase wall ms (with device syncs)
+        self._t_mark = self._t_sub = 0.0
 
     # ------------------------------------------------------------ views
     @property
@@ -147,14 +148,13 @@ class DeviceGA:
             self.store[:n] = genomes.to(device=self.device, dtype=self.dtype)
         self.hof_n = n
         self._hof_fit_host = fit.copy()
-        self._hof_hash_host = D.row_hash(self.store[:n], self.G).cpu().numpy() if n else np.zeros(0, np.int64)
         if n:
             self.hof_fitness[:n] = torch.from_numpy(fit).to(self.device)
+            self.hof_hash[:n] = D.row_hash(self.store[:n], self.G)
 
     def _set_hof_empty(self):
         self.hof_n = 0
         self._hof_fit_host = np.zeros(0, np.float64)
-        self._hof_hash_host = np.zeros(0, np.int64)
 
     # ------------------------------------------------------------ steps
     def _evaluate(self, g: int, rows: torch.Tensor) -> torch.Tensor:
@@ -196,24 +196,45 @@ class DeviceGA:
         if k == 0:
             dst[:old_n] = self.store[:old_n]
             return
-        cand32 = cand.to(torch.int32)
-        h = D.row_hash(rows, self.G, index=cand32).cpu().numpy()
-        f = fit[cand].cpu().numpy()
-        src, new_fit = D.hof_update(self.H, self._hof_fit_host, self._hof_hash_host, f, h)
+        h = D.row_hash(rows, self.G, index=cand.to(torch.int32))
+        fc = fit[cand]
+        # Everything the sequential scan needs, computed on the device and sent
+        # in one copy: each entry's rank in ascending (fitness, age) order (in
+        # age order the old members come oldest first, then the candidates), a
+        # dense similarity class per entry, and the candidates' fitness.
+        n = old_n + k
+        if self.profile is not None:
+            self.profile["hof_candidates"] = self.profile.get("hof_candidates", 0) + k
+        by_age = torch.cat([self.hof_fitness[:old_n].flip(0), fc])
+        order = torch.sort(by_age, stable=True).indices
+        rank_age = torch.empty_like(order)
+        rank_age[order] = torch.arange(n, device=self.device)
+        rank = torch.cat([rank_age[:old_n].flip(0), rank_age[old_n:]])
+        hashes = torch.cat([self.hof_hash[:old_n], h])
+        cls = torch.unique(hashes, return_inverse=True)[1]
+        packed = torch.cat([rank | (cls << 32), fc.view(torch.int64)]).cpu().numpy()
+        self._mark("hof_prepare", sub=True)
+        rank_np = (packed[:n] & 0xFFFFFFFF).astype(np.int32)
+        cls_np = packed[:n] >> 32
+        src, new_fit = D.hof_update(self.H, self._hof_fit_host, cls_np[:old_n], packed[n:].view(np.float64),
+                                    cls_np[old_n:], rank=rank_np)
+        self._mark("hof_scan", sub=True)
+        m = src.shape[0]
         is_old = src < old_n
-        src_t = torch.from_numpy(src.astype(np.int64)).to(self.device)
-        old_t = torch.from_numpy(is_old).to(self.device)
-        pos = torch.arange(src.shape[0], device=self.device)
-        if is_old.any():
-            dst[pos[old_t]] = self.store[src_t[old_t]]
-        if (~is_old).any():
-            dst[pos[~old_t]] = rows[cand[src_t[~old_t] - old_n]]
-        hashes = np.empty(src.shape[0], np.int64)
-        hashes[is_old] = self._hof_hash_host[src[is_old]]
-        hashes[~is_old] = h[src[~is_old] - old_n]
-        self.hof_n = int(src.shape[0])
-        self._hof_fit_host, self._hof_hash_host = new_fit, hashes
-        self.hof_fitness[: self.hof_n] = torch.from_numpy(new_fit).to(self.device)
+        pos_old, pos_new = np.nonzero(is_old)[0], np.nonzero(~is_old)[0]
+        idx = torch.from_numpy(np.concatenate([pos_old, src[pos_old], pos_new, src[pos_new] - old_n,
+                                               np.arange(m), src]).astype(np.int64)).to(self.device)
+        a, b = pos_old.size, pos_old.size * 2
+        c = b + pos_new.size
+        d = c + pos_new.size
+        if a:
+            dst.index_copy_(0, idx[:a], self.store.index_select(0, idx[a:b]))
+        if c > b:
+            dst.index_copy_(0, idx[b:c], rows.index_select(0, cand.index_select(0, idx[c:d])))
+        self.hof_hash[:m] = hashes.index_select(0, idx[d + m:])
+        self.hof_n = int(m)
+        self._hof_fit_host = new_fit
+        self.hof_fitness[:m] = torch.from_numpy(new_fit).to(self.device)
 
     def _record(self, g: int, nevals: int) -> dict:
         f = self.fitness
@@ -256,15 +277,21 @@ class DeviceGA:
         self._mark("record")
         return rec
 
-    def _mark(self, phase):
+    def _mark(self, phase, sub: bool = False):
+        """Profiling: add the wall time since the last top-level mark to
+        ``phase``; ``sub`` marks split a phase (since the last mark of either kind)."""
         if self.profile is None:
             return
         import time
         torch.cuda.synchronize(self.device)
         now = time.perf_counter()
+        if sub:
+            self.profile[phase] = self.profile.get(phase, 0.0) + (now - self._t_sub) * 1e3
+            self._t_sub = now
+            return
         if phase is not None:
             self.profile[phase] = self.profile.get(phase, 0.0) + (now - self._t_mark) * 1e3
-        self._t_mark = now
+        self._t_mark = self._t_sub = now
 
     def run(self, ngen: int, verbose: bool = False) -> list:
         """algorithms.eaSimple(..., ngen): the initial evaluation if pending, then ngen generations."""

@@ -27,8 +27,19 @@ def _mk(Ind, h, f):
     return ind
 
 
+def _ranks(keys_f, fit):
+    """pg_hof_args.rank as DeviceGA._hof_update computes it: a stable sort in age order."""
+    by_age = np.concatenate([np.asarray(keys_f, np.float64)[::-1], np.asarray(fit, np.float64)])
+    order = np.argsort(by_age, kind="stable")
+    rank_age = np.empty(order.size, np.int32)
+    rank_age[order] = np.arange(order.size)
+    n_old = len(keys_f)
+    return np.concatenate([rank_age[:n_old][::-1], rank_age[n_old:]])
+
+
+@pytest.mark.parametrize("given_rank", [False, True])
 @pytest.mark.parametrize("seed", range(12))
-def test_hof_update_matches_deap_restatement(Ind, seed):
+def test_hof_update_matches_deap_restatement(Ind, seed, given_rank):
     rng = np.random.default_rng(seed)
     maxsize = int(rng.integers(1, 24))
     hof = tools.HallOfFame(maxsize)
@@ -40,7 +51,8 @@ def test_hof_update_matches_deap_restatement(Ind, seed):
         hsh = rng.integers(-2**62, 2**62, size=8)[rng.integers(0, 8, size=n)]
         pop = [_mk(Ind, h, f) for h, f in zip(hsh, fit)]
         hof.update(pop)
-        src, new_fit = D.hof_update(maxsize, keys_f, keys_h, fit, hsh)
+        src, new_fit = D.hof_update(maxsize, keys_f, keys_h, fit, hsh,
+                                    rank=_ranks(keys_f, fit) if given_rank else None)
         old_n = keys_f.shape[0]
         new_h = np.array([keys_h[s] if s < old_n else hsh[s - old_n] for s in src], dtype=np.int64)
         assert [i.fitness.values[0] for i in hof] == list(new_fit)
@@ -67,6 +79,8 @@ def test_hof_update_rejects_bad_arguments():
         D.hof_update(1, [1.0, 2.0], [1, 2], [], [])  # more members than maxsize
     with pytest.raises(ValueError):
         D.hof_update(3, [1.0], [], [], [])
+    with pytest.raises(_lib.PongGAError):
+        D.hof_update(3, [1.0], [1], [2.0], [2], rank=[0, 2])  # rank out of range
 
 
 def test_hof_update_large_is_fast():
