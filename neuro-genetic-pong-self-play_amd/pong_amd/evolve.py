@@ -83,6 +83,7 @@ class DeviceGA:
         self.eval_events = None  # optional (start, end) HIP events recorded around the evaluation launch
         self.profile = None      # dict: when set, step() adds per-phase wall ms (with device syncs)
         self._t_mark = self._t_sub = 0.0
+        self._next = None        # (generation, inv, inherited): offspring already varied into spare[H:]
 
     # ------------------------------------------------------------ views
     @property
@@ -117,6 +118,7 @@ class DeviceGA:
         self.valid.zero_()
         self.fitness.zero_()
         self._set_hof_empty()
+        self._next = None
         self.generation = -1
         self.logbook = []
 
@@ -125,6 +127,7 @@ class DeviceGA:
         """Load P genomes (and, for individuals whose fitness is valid, their fitness)."""
         if tuple(genomes.shape) != (self.P, self.G):
             raise ValueError(f"genomes must be [{self.P}, {self.G}], got {tuple(genomes.shape)}")
+        self._next = None
         self.population.copy_(genomes.to(device=self.device, dtype=self.dtype))
         if fitness is None:
             self.valid.zero_()
@@ -180,10 +183,23 @@ class DeviceGA:
         if bool(torch.isnan(fit).any()):
             raise ZeroDivisionError("float division by zero (calculate_reward with total_frames == 0)")
 
-    def _hof_update(self, fit: torch.Tensor, rows: torch.Tensor, dst: torch.Tensor):
+    def _select_vary(self, g: int, parents: torch.Tensor, fitness: torch.Tensor, out: torch.Tensor):
+        """Generation g's selTournament + varAnd into ``out``: returns (inv, inherited)."""
+        chosen = D.select_tournament_ranked(fitness, self.P, self.tournsize, seed=self.seed, generation=g)
+        _, invalid = D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu,
+                            self.sigma, self.indpb, seed=self.seed, generation=g, out=out)
+        inherited = fitness[chosen.long()]  # a clone keeps its parent's fitness (varAnd)
+        return invalid.bool(), inherited
+
+    def _hof_update(self, fit: torch.Tensor, rows: torch.Tensor, dst: torch.Tensor, overlap=None):
         """HallOfFame.update(rows) with fitness ``fit``; the members are gathered
-        into dst[:new_n] (dst is disjoint from the current members and rows)."""
+        into dst[:new_n] (dst is disjoint from the current members and rows).
+        ``overlap`` (a callable enqueueing device work that touches none of
+        these rows) runs once the host scan's inputs are copied out, so the
+        device executes it while the host scans."""
         if self.H == 0:
+            if overlap:
+                overlap()
             return
         old_n = self.hof_n
         if old_n >= self.H:
@@ -195,6 +211,8 @@ class DeviceGA:
         k = int(cand.numel())
         if k == 0:
             dst[:old_n] = self.store[:old_n]
+            if overlap:
+                overlap()
             return
         h = D.row_hash(rows, self.G, index=cand.to(torch.int32))
         fc = fit[cand]
@@ -212,7 +230,15 @@ class DeviceGA:
         rank = torch.cat([rank_age[:old_n].flip(0), rank_age[old_n:]])
         hashes = torch.cat([self.hof_hash[:old_n], h])
         cls = torch.unique(hashes, return_inverse=True)[1]
-        packed = torch.cat([rank | (cls << 32), fc.view(torch.int64)]).cpu().numpy()
+        packed_d = torch.cat([rank | (cls << 32), fc.view(torch.int64)])
+        packed_h = torch.empty(packed_d.shape, dtype=torch.int64, pin_memory=True)
+        packed_h.copy_(packed_d, non_blocking=True)
+        copied = torch.cuda.Event()
+        copied.record()
+        if overlap:
+            overlap()
+        copied.synchronize()
+        packed = packed_h.numpy()
         self._mark("hof_prepare", sub=True)
         rank_np = (packed[:n] & 0xFFFFFFFF).astype(np.int32)
         cls_np = packed[:n] >> 32
@@ -251,24 +277,29 @@ class DeviceGA:
             new_fit = torch.where(self.valid, self.fitness, fit)
             self._check(new_fit)
             self.fitness, self.valid = new_fit, torch.ones_like(self.valid)
-            self._hof_update(new_fit, self.population, self.spare)
+            # generation 1's offspring go to spare[H:] (no swap after the initial update)
+            self._hof_update(new_fit, self.population, self.spare,
+                             overlap=lambda: self._prefetch(1, self.population, new_fit, self.spare))
             self.store[: self.hof_n] = self.spare[: self.hof_n]
             self.generation = 0
             return self._record(0, nevals)
         g = self.generation + 1
         self._mark(None)
-        chosen = D.select_tournament_ranked(self.fitness, self.P, self.tournsize, seed=self.seed, generation=g)
         off = self.spare[self.H:]
-        _, invalid = D.vary(self.population, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu,
-                            self.sigma, self.indpb, seed=self.seed, generation=g, out=off)
-        inv = invalid.bool()
-        inherited = self.fitness[chosen.long()]  # a clone keeps its parent's fitness (varAnd)
+        if self._next is not None and self._next[0] == g:
+            inv, inherited = self._next[1:]  # selected and varied during the previous hall-of-fame scan
+        else:
+            inv, inherited = self._select_vary(g, self.population, self.fitness, off)
+        self._next = None
         self._mark("select_vary")
         fit = self._evaluate(g, off)
         new_fit = torch.where(inv, fit, inherited)
         self._mark("evaluate")
         self._check(new_fit)
-        self._hof_update(new_fit, off, self.spare)
+        # generation g + 1's parents are this offspring; its offspring go to
+        # store[H:] (this generation's parents, free now), the buffer the swap
+        # below makes next step's spare[H:]
+        self._hof_update(new_fit, off, self.spare, overlap=lambda: self._prefetch(g + 1, off, new_fit, self.store))
         self._mark("hall_of_fame")
         self.fitness = new_fit
         self.store, self.spare = self.spare, self.store
@@ -276,6 +307,9 @@ class DeviceGA:
         rec = self._record(g, int(inv.sum()))
         self._mark("record")
         return rec
+
+    def _prefetch(self, g: int, parents: torch.Tensor, fitness: torch.Tensor, store: torch.Tensor):
+        self._next = (g,) + self._select_vary(g, parents, fitness, store[self.H:])
 
     def _mark(self, phase, sub: bool = False):
         """Profiling: add the wall time since the last top-level mark to

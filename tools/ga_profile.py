@@ -30,3 +30,11 @@ for s in range(steps):
     ms = (time.perf_counter() - t0) * 1e3
     print(f"gen {rec['gen']}: {ms:.2f} ms  " + "  ".join(f"{k} {v:.2f}" for k, v in ga.profile.items())
           + f"  nevals {rec['nevals']} hof_n {ga.hof_n}", flush=True)
+
+ga.profile = None
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for s in range(steps):
+    ga.step()
+torch.cuda.synchronize()
+print(f"unprofiled: {(time.perf_counter() - t0) * 1e3 / steps:.2f} ms per generation over {steps}", flush=True)
