@@ -73,11 +73,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PG_DIST_BACKEND=gloo with more ranks than GPUs: a rehearsal of the N > 1
+    # path on a one-GPU box (ranks share devices); the driver's runs use RCCL
+    backend = os.environ.get("PG_DIST_BACKEND", "nccl")
+    local_dev = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local_dev if world > 1 else 0)
     torch.cuda.set_device(dev)
 
     from pong_amd import build as B
@@ -174,7 +181,7 @@ def main():
     if rank == 0 and args.config == "wide":
         out = wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all,
                           passes_all, kernel_ms_mean, skip_all)
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline: rank 0 at N=1 only
             out["cpu_baseline"] = cpu_baseline(args, shape, ga, chunk=8,
                                               max_rows=256)
         print(json.dumps(out), flush=True)
@@ -229,7 +236,7 @@ def main():
                          "streaming_equivalent_GBps": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9,
                          "streaming_equivalent_frac_of_hbm": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9 / HBM_PEAK_GBS},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline: rank 0 at N=1 only
             out["cpu_baseline"] = cpu_baseline(args, shape, ga)
         print(json.dumps(out), flush=True)
     if world > 1:
