@@ -1126,8 +1126,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifndef PG_NO_RALLY_SKIP
     // a periodic rally ends at the timeout with nothing else changed: jump there
     // (never while tracing, which records every frame's actions)
+#ifdef PG_TIMELINE
+    constexpr bool kTracing = false;  // the timeline build's trace buffer holds stamps, not actions
+#else
+    const bool kTracing = p.trace != nullptr;
+#endif
     if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
-        !p.trace) {
+        !kTracing) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
       const uint64_t key = rally_key(st, act_r, act_l);
       if (timeout == kRallyStart) {
