@@ -86,6 +86,27 @@ __global__ __launch_bounds__(256) void k_render(const int32_t *state, int n, uin
 // find_stuff for one frame per workgroup: per-channel match counts and row /
 // column sums of the ball, left and right colours over the crop, reduced
 // exactly in integers, then mean = sum / count in f64 (NaN = None).
+//
+// Byte compares four at a time (SWAR): word j of a 16-pixel group holds bytes
+// 4j..4j+3, i.e. fixed (pixel, channel) slots, so colour k's expected word is
+// a constant E_k[j % 3].  x = w ^ E has a zero byte exactly where a channel
+// matches; ((x & 0x7F..) + 0x7F..) | x has the high bit of every NONZERO byte
+// set (exact, no carries between bytes).  The group's misses are counted with
+// v_bcnt and their pixel indices summed with v_dot4_u32_u8 against the
+// constant per-byte pixel index of word j; matches = 48 - misses, index sum =
+// 360 - weighted misses.
+__host__ __device__ constexpr uint32_t fs_expected(int k, int j) {  // k: 1..3 (ball, left, right)
+  constexpr uint8_t c[4][3] = {{144, 72, 17}, {236, 236, 236}, {213, 130, 74}, {92, 186, 92}};
+  uint32_t w = 0;
+  for (int b = 0; b < 4; ++b) w |= (uint32_t)c[k][(4 * j + b) % 3] << (8 * b);
+  return w;
+}
+__host__ __device__ constexpr uint32_t fs_pixel_index(int j) {  // pixel of each byte of word j, x 128
+  uint32_t w = 0;
+  for (int b = 0; b < 4; ++b) w |= (uint32_t)((4 * j + b) / 3) << (8 * b);
+  return w;
+}
+
 __global__ __launch_bounds__(256) void k_find_stuff(const uint8_t *frames, int64_t stride, int n, double *out) {
   __shared__ int part[4][9];
   const int f = blockIdx.x;
@@ -98,26 +119,21 @@ __global__ __launch_bounds__(256) void k_find_stuff(const uint8_t *frames, int64
     const uint4 a = src[0], b = src[1], c = src[2];
     const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
     const int row = g / (kFrameW / kGroupPix), col0 = (g % (kFrameW / kGroupPix)) * kGroupPix;
-    int m[3] = {0, 0, 0}, mx[3] = {0, 0, 0};  // matches and sum of (match x pixel index in group)
-#pragma unroll
-    for (int i = 0; i < kGroupPix; ++i) {
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        const int bi = 3 * i + ch;
-        const uint32_t v = (w[bi >> 2] >> (8 * (bi & 3))) & 0xFFu;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int hit = v == kColours[k + 1][ch];
-          m[k] += hit;
-          mx[k] += hit * i;
-        }
-      }
-    }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      cnt[k] += m[k];
-      rs[k] += m[k] * row;
-      cs[k] += m[k] * col0 + mx[k];
+      uint32_t miss = 0, wmiss = 0;  // missed bytes; their pixel indices x 128
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        const uint32_t x = w[j] ^ fs_expected(k + 1, j % 3);
+        const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+        miss += __builtin_popcount(nz);
+        wmiss = __builtin_amdgcn_udot4(nz, fs_pixel_index(j), wmiss, false);
+      }
+      const int m = 48 - (int)miss;
+      const int mx = 360 - (int)(wmiss >> 7);
+      cnt[k] += m;
+      rs[k] += m * row;
+      cs[k] += m * col0 + mx;
     }
   }
   int v[9] = {cnt[0], cnt[1], cnt[2], rs[0], rs[1], rs[2], cs[0], cs[1], cs[2]};
