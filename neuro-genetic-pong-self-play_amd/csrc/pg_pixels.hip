@@ -50,8 +50,23 @@ __device__ __forceinline__ int pixel_colour(const FrameState &s, int row, int co
   return c;
 }
 
-// One workgroup per frame; a thread writes 16-pixel groups as three 16-B stores.
+// Word j of a 16-pixel group painted in one colour (bytes 4j..4j+3 are fixed
+// (pixel, channel) slots, so the pattern repeats every three words).
+__device__ __forceinline__ uint32_t solid_word(int c, int j) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) w |= (uint32_t)kColours[c][(4 * j + b) % 3] << (8 * b);
+  return w;
+}
+
+// One workgroup per frame; a thread paints a 16-pixel group (48 B, a group
+// never crosses a row).  Most groups hold no object (one solid colour:
+// background or wall) and come from three constant words; only groups an
+// object's rectangle touches take the per-pixel path.  The wave's 64 groups
+// (3 KB contiguous) are transposed through LDS so that each of its three
+// 16-B stores covers 1 KB contiguously.
 __global__ __launch_bounds__(256) void k_render(const int32_t *state, int n, uint8_t *frames) {
+  __shared__ uint4 stage[4][192];  // per wave: 64 groups x 3 pieces
   const int f = blockIdx.x;
   if (f >= n) return;
   FrameState s;
@@ -60,26 +75,45 @@ __global__ __launch_bounds__(256) void k_render(const int32_t *state, int n, uin
   s.vis = state[PG_S_BALL_VISIBLE * (long)n + f];
   s.lpy = state[PG_S_LEFT_Y * (long)n + f];
   s.rpy = state[PG_S_RIGHT_Y * (long)n + f];
-  uint8_t *out = frames + (long)f * kFrameBytes;
+  uint4 *out = (uint4 *)(frames + (long)f * kFrameBytes);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int kGroups = kFrameH * kFrameW / kGroupPix;  // 2100
-  for (int g = threadIdx.x; g < kGroups; g += blockDim.x) {
+  for (int g0 = threadIdx.x - lane; g0 < kGroups; g0 += blockDim.x) {
+    const int g = g0 + lane;
     const int row = g / (kFrameW / kGroupPix), col0 = (g % (kFrameW / kGroupPix)) * kGroupPix;
+    const int fr = row - kCropTop;
+    const bool in_crop = fr >= 0 && fr < kCropRows;
+    const auto spans = [&](int x0, int w) { return x0 < col0 + kGroupPix && x0 + w > col0; };
+    const bool lp = spans(kLeftPaddleX, kPaddleW) && fr >= s.lpy && fr <= s.lpy + kPaddleH - 1;
+    const bool rp = spans(kRightPaddleX, kPaddleW) && fr >= s.rpy && fr <= s.rpy + kPaddleH - 1;
+    const bool ball = s.vis && fr >= s.by && fr < s.by + kBallH && spans(s.bx, kBallW);
     uint32_t w[12];
+    if (g < kGroups && in_crop && (lp || rp || ball)) {
 #pragma unroll
-    for (int q = 0; q < 12; ++q) w[q] = 0;
+      for (int q = 0; q < 12; ++q) w[q] = 0;
 #pragma unroll
-    for (int i = 0; i < kGroupPix; ++i) {
-      const int c = pixel_colour(s, row, col0 + i);
+      for (int i = 0; i < kGroupPix; ++i) {
+        const int c = pixel_colour(s, row, col0 + i);
 #pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        const int b = 3 * i + ch;  // byte within the group, static
-        w[b >> 2] |= (uint32_t)kColours[c][ch] << (8 * (b & 3));
+        for (int ch = 0; ch < 3; ++ch) {
+          const int b = 3 * i + ch;  // byte within the group, static
+          w[b >> 2] |= (uint32_t)kColours[c][ch] << (8 * (b & 3));
+        }
       }
+    } else {  // the group's colour: pixel_colour without objects
+      const bool wall = (row >= 24 && row < kCropTop) || row >= kCropTop + kCropRows;
+#pragma unroll
+      for (int q = 0; q < 12; ++q) w[q] = wall ? solid_word(1, q % 3) : solid_word(0, q % 3);
     }
-    uint4 *dst = (uint4 *)(out + (long)g * kGroupBytes);
-    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+    stage[wave][3 * lane] = make_uint4(w[0], w[1], w[2], w[3]);
+    stage[wave][3 * lane + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+    stage[wave][3 * lane + 2] = make_uint4(w[8], w[9], w[10], w[11]);
+    wave_lds_sync();
+    const int pieces = 3 * (kGroups - g0 < 64 ? kGroups - g0 : 64);  // 16-B pieces of this wave's groups
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      if (64 * k + lane < pieces) out[3 * g0 + 64 * k + lane] = stage[wave][64 * k + lane];
+    wave_lds_sync();
   }
 }
 
