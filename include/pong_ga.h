@@ -35,6 +35,7 @@
  * pg_row_hash                    DEAP HallOfFame's similar (operator.eq on the
  *                                gene lists, ga.py:78) as a 64-bit row hash
  * pg_hof_update (host)           tools.HallOfFame.update (eaSimple, main.py:165-170)
+ * pg_gather_rows                 the new hall's genomes (HallOfFame.insert's deepcopy)
  * pg_render_frames               the frame env.step returns (main.py:77; the build's
  *                                rasteriser of its SoA state in config.py colours)
  * pg_find_stuff                  find_stuff utils.py:14-19 / get_rect_quickly
@@ -271,6 +272,12 @@ int32_t pg_row_hash(const void *rows, int64_t stride, const int32_t *index, int3
                     int32_t dtype, uint64_t *hash, void *stream);
 /* Host only (no device memory, no GPU needed). */
 int32_t pg_hof_update(const pg_hof_args *args);
+/* dst row j = old_rows[src[j]] if src[j] < n_old, else rows[index[src[j] - n_old]]
+ * (index NULL: rows[src[j] - n_old]) -- pg_hof_update's new_src applied in one
+ * pass; strides in elements, dst disjoint from both sources. */
+int32_t pg_gather_rows(void *dst, int64_t dst_stride, const void *old_rows, int64_t old_stride, const void *rows,
+                       int64_t rows_stride, const int64_t *index, const int32_t *src, int32_t n_old, int32_t n,
+                       int64_t genes, int32_t dtype, void *stream);
 /* frames [n, 210, 160, 3] uint8 (16-byte aligned) from the SoA state [PG_STATE_FIELDS, n]:
  * background, the walls above/below the playfield, both paddles, the ball if visible. */
 int32_t pg_render_frames(const int32_t *state, int32_t n, uint8_t *frames, void *stream);

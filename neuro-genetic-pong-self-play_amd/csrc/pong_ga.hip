@@ -1483,6 +1483,19 @@ __global__ void k_schedule(pg_schedule_args a) {
   a.mult[w] = mult;
 }
 
+// pg_gather_rows: one workgroup per destination row.
+template <typename WT>
+__global__ __launch_bounds__(256) void k_gather_rows(WT *dst, int64_t dst_stride, const WT *old_rows, int64_t old_stride,
+                                                     const WT *rows, int64_t rows_stride, const int64_t *index,
+                                                     const int32_t *src, int n_old, int64_t genes) {
+  const int j = blockIdx.x;
+  const int s = src[j];
+  const WT *from = s < n_old ? old_rows + (long)s * old_stride
+                             : rows + (index ? index[s - n_old] : (long)(s - n_old)) * rows_stride;
+  WT *to = dst + (long)j * dst_stride;
+  for (int64_t g = threadIdx.x; g < genes; g += 256) to[g] = from[g];
+}
+
 // 64-bit content hash of each row: an order-independent sum of mixed
 // (index, bit pattern) terms, so the block reduction order cannot matter.
 template <typename WT>
@@ -1918,6 +1931,26 @@ int32_t pg_ga_schedule(const pg_schedule_args *a, void *stream) {
     return fail(PG_ERR_INVALID, "schedule: NULL output or hof_fitness");
   const long total = (long)a->n * a->n_games;
   hipLaunchKernelGGL(k_schedule, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *a);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_gather_rows(void *dst, int64_t dst_stride, const void *old_rows, int64_t old_stride, const void *rows,
+                       int64_t rows_stride, const int64_t *index, const int32_t *src, int32_t n_old, int32_t n,
+                       int64_t genes, int32_t dtype, void *stream) {
+  if (n < 0 || n_old < 0 || genes < 1 || (dtype != PG_F32 && dtype != PG_F64) ||
+      (n > 0 && (!dst || !src || (n_old > 0 && !old_rows) || dst_stride < genes || old_stride < genes ||
+                 rows_stride < genes)))
+    return fail(PG_ERR_INVALID, "gather_rows: bad sizes, dtype or NULL buffers");
+  if (n == 0) return PG_OK;
+  if (dtype == PG_F64)
+    hipLaunchKernelGGL(k_gather_rows<double>, dim3(n), dim3(256), 0, (hipStream_t)stream, (double *)dst, dst_stride,
+                       (const double *)old_rows, old_stride, (const double *)rows, rows_stride, index, src, n_old,
+                       genes);
+  else
+    hipLaunchKernelGGL(k_gather_rows<float>, dim3(n), dim3(256), 0, (hipStream_t)stream, (float *)dst, dst_stride,
+                       (const float *)old_rows, old_stride, (const float *)rows, rows_stride, index, src, n_old,
+                       genes);
   PG_HIP(hipGetLastError());
   return PG_OK;
 }

@@ -117,6 +117,8 @@ SIGNATURES = {
     "pg_row_hash": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp,
                                      _vp]),
     "pg_hof_update": (ctypes.c_int32, [ctypes.POINTER(PgHofArgs)]),
+    "pg_gather_rows": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, _vp,
+                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp]),
     "pg_render_frames": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp]),
     "pg_find_stuff": (ctypes.c_int32, [_vp, ctypes.c_int64, ctypes.c_int32, _vp, _vp]),
 }

@@ -316,6 +316,28 @@ def row_hash(rows: torch.Tensor, genes: Optional[int] = None, index: Optional[to
     return out
 
 
+def gather_rows(dst: torch.Tensor, old_rows: torch.Tensor, rows: torch.Tensor, src: torch.Tensor, n_old: int,
+                index: Optional[torch.Tensor] = None, genes: Optional[int] = None) -> torch.Tensor:
+    """pg_gather_rows: dst[j] = old_rows[src[j]] if src[j] < n_old else
+    rows[index[src[j] - n_old]] (rows[src[j] - n_old] without index)."""
+    dev = dst.device
+    n = src.shape[0]
+    _need(src, "src", torch.int32, dev, (n,))
+    if index is not None:
+        _need(index, "index", torch.int64, dev, (index.shape[0],))
+    for name, t in (("dst", dst), ("old_rows", old_rows), ("rows", rows)):
+        if t.dim() != 2 or t.dtype != dst.dtype or t.device != dev or t.stride(1) != 1:
+            raise ValueError(f"{name} must be a row-major [n, G] tensor of dst's dtype on dst's device")
+    genes = dst.shape[1] if genes is None else int(genes)
+    if n > dst.shape[0]:
+        raise ValueError("more source indices than destination rows")
+    with torch.cuda.device(dev):
+        L.check("pg_gather_rows", L.lib().pg_gather_rows(
+            _ptr(dst), dst.stride(0), _ptr(old_rows), old_rows.stride(0), _ptr(rows), rows.stride(0), _ptr(index),
+            _ptr(src), int(n_old), n, genes, DTYPES[dst.dtype], _stream(dev)))
+    return dst
+
+
 def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash, rank=None):
     """pg_hof_update (host, no GPU): HallOfFame.update over fitness/hash arrays.
 

@@ -246,21 +246,18 @@ class DeviceGA:
                                     cls_np[old_n:], rank=rank_np)
         self._mark("hof_scan", sub=True)
         m = src.shape[0]
-        is_old = src < old_n
-        pos_old, pos_new = np.nonzero(is_old)[0], np.nonzero(~is_old)[0]
-        idx = torch.from_numpy(np.concatenate([pos_old, src[pos_old], pos_new, src[pos_new] - old_n,
-                                               np.arange(m), src]).astype(np.int64)).to(self.device)
-        a, b = pos_old.size, pos_old.size * 2
-        c = b + pos_new.size
-        d = c + pos_new.size
-        if a:
-            dst.index_copy_(0, idx[:a], self.store.index_select(0, idx[a:b]))
-        if c > b:
-            dst.index_copy_(0, idx[b:c], rows.index_select(0, cand.index_select(0, idx[c:d])))
-        self.hof_hash[:m] = hashes.index_select(0, idx[d + m:])
+        # one pinned upload: the members' fitness bits, then their sources
+        up = torch.empty(3 * m, dtype=torch.int32, pin_memory=True)
+        upn = up.numpy()
+        upn[: 2 * m].view(np.float64)[:] = new_fit
+        upn[2 * m:] = src
+        up_d = up.to(self.device, non_blocking=True)
+        src_t = up_d[2 * m:]
+        D.gather_rows(dst, self.store, rows, src_t, old_n, index=cand)
+        self.hof_hash[:m] = hashes.index_select(0, src_t.long())
+        self.hof_fitness[:m] = up_d[: 2 * m].view(torch.float64)
         self.hof_n = int(m)
         self._hof_fit_host = new_fit
-        self.hof_fitness[:m] = torch.from_numpy(new_fit).to(self.device)
 
     def _record(self, g: int, nevals: int) -> dict:
         f = self.fitness

@@ -112,3 +112,23 @@ def test_vary_mutpb_fraction_and_f32(gpu):
     changed = (off != par).any(dim=1).cpu().numpy()
     assert abs(changed.mean() - 0.4) < 0.03
     np.testing.assert_array_equal(changed, inv.cpu().numpy().astype(bool))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gather_rows_applies_hof_sources(gpu, dtype):
+    """pg_gather_rows: dst[j] = old[src[j]] below n_old, else rows[index[src[j] - n_old]]."""
+    from pong_amd import device as D
+    rng = np.random.default_rng(5)
+    G, n_old, n_rows = 643, 37, 90
+    store = torch.randn((n_old + 200, G + 5), dtype=torch.float64, device=gpu).to(dtype)  # wider stride
+    rows = torch.randn((n_rows, G), dtype=torch.float64, device=gpu).to(dtype)
+    cand = torch.tensor(rng.permutation(n_rows)[:50], dtype=torch.int64, device=gpu)
+    src = rng.integers(0, n_old + 50, size=61).astype(np.int32)
+    dst = torch.zeros((64, G), dtype=dtype, device=gpu)
+    D.gather_rows(dst, store, rows, torch.tensor(src, device=gpu), n_old, index=cand, genes=G)
+    want = torch.stack([store[s, :G] if s < n_old else rows[cand[s - n_old]] for s in src.tolist()])
+    assert torch.equal(dst[:61], want) and bool((dst[61:] == 0).all())
+    # without an index the population entry is the row itself
+    D.gather_rows(dst, store, rows, torch.tensor(src, device=gpu), n_old, genes=G)
+    want = torch.stack([store[s, :G] if s < n_old else rows[s - n_old] for s in src.tolist()])
+    assert torch.equal(dst[:61], want)

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out/s7
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_ga.py tests/test_gpu_evolve.py tests/test_gpu_dist.py tests/test_gpu_replay.py > gpurun_out/s7/tests.log 2>&1 || exit 1
+timeout -k 10 600 python -u tools/ga_profile.py 524288 4 > gpurun_out/s7/profile_524k.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/ga_profile.py 65536 6 > gpurun_out/s7/profile_65k.log 2>&1 || exit 1
