@@ -1404,54 +1404,67 @@ __device__ __forceinline__ uint64_t rng_key(uint64_t seed, uint64_t gen, uint64_
 __device__ __forceinline__ double rng_u01(uint64_t key, uint64_t b) {
   return (double)(splitmix64(key ^ b) >> 11) * 0x1.0p-53;
 }
-__device__ __forceinline__ float rng_u01f(uint64_t key, uint64_t b) {
-  return (float)(splitmix64(key ^ b) >> 40) * 0x1.0p-24f;
-}
 
+// One wave per pair: the pair's draws (crossover, mutation, the keys of its
+// per-gene streams) are wave-uniform scalar work done once, then the wave
+// sweeps the genes 128 at a time (two coalesced 512-B pieces per parent row,
+// all four loads issued before the arithmetic).
 template <typename WT>
-__global__ void k_vary(pg_ga_args a) {
-  const long gene = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gene >= a.genes) return;
-  const WT *par = (const WT *)a.parents;
-  WT *off = (WT *)a.offspring;
+__global__ __launch_bounds__(256) void k_vary(pg_ga_args a) {
   const int pairs = (a.n + 1) / 2;
-  for (int pair = blockIdx.y; pair < pairs; pair += gridDim.y) {  // individuals 2*pair, 2*pair + 1
-    const int i0 = 2 * pair, i1 = 2 * pair + 1;
-    const bool has1 = i1 < a.n;
-    double x1 = (double)par[(long)a.chosen[i0] * a.stride + gene];
-    double x2 = has1 ? (double)par[(long)a.chosen[i1] * a.stride + gene] : 0.0;
-    const bool cx = has1 && rng_u01(rng_key(a.seed, a.generation, 2, (uint64_t)pair), 0) < a.cxpb;
+  const int pair = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (pair >= pairs) return;
+  const int lane = threadIdx.x & 63;
+  const int i0 = 2 * pair, i1 = 2 * pair + 1;
+  const bool has1 = i1 < a.n;
+  const bool cx = has1 && rng_u01(rng_key(a.seed, a.generation, 2, (uint64_t)pair), 0) < a.cxpb;
+  const uint64_t k3 = rng_key(a.seed, a.generation, 3, (uint64_t)pair);
+  const bool mut0 = rng_u01(rng_key(a.seed, a.generation, 4, (uint64_t)i0), 0) < a.mutpb;
+  const bool mut1 = has1 && rng_u01(rng_key(a.seed, a.generation, 4, (uint64_t)i1), 0) < a.mutpb;
+  const uint64_t k5 = rng_key(a.seed, a.generation, 5, (uint64_t)pair);
+  const uint64_t k6 = rng_key(a.seed, a.generation, 6, (uint64_t)pair);
+  const WT *p1 = (const WT *)a.parents + (long)a.chosen[i0] * a.stride;
+  const WT *p2 = (const WT *)a.parents + (long)(has1 ? a.chosen[i1] : a.chosen[i0]) * a.stride;
+  WT *o1 = (WT *)a.offspring + (long)i0 * a.stride;
+  WT *o2 = (WT *)a.offspring + (long)i1 * a.stride;
+  const auto one = [&](long gene, double x1, double x2) {
     if (cx) {
-      const double u = rng_u01(rng_key(a.seed, a.generation, 3, (uint64_t)pair), (uint64_t)gene);
+      const double u = rng_u01(k3, (uint64_t)gene);
       const double gamma = __dadd_rn(__dmul_rn(1.0 + 2.0 * a.alpha, u), -a.alpha);
       const double y1 = __dadd_rn(__dmul_rn(1.0 - gamma, x1), __dmul_rn(gamma, x2));
       const double y2 = __dadd_rn(__dmul_rn(gamma, x1), __dmul_rn(1.0 - gamma, x2));
       x1 = y1;
       x2 = y2;
     }
-    bool mut[2], hit[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const uint64_t ind = (uint64_t)(i0 + s);
-      mut[s] = (s == 0 || has1) && rng_u01(rng_key(a.seed, a.generation, 4, ind), 0) < a.mutpb;
-      hit[s] = mut[s] && rng_u01(rng_key(a.seed, a.generation, 5, ind), (uint64_t)gene) < a.indpb;
-    }
-    if (hit[0] || hit[1]) {
-      const uint64_t kb = rng_key(a.seed, a.generation, 6, (uint64_t)pair);
-      const float u1 = 1.0f - rng_u01f(kb, 2 * (uint64_t)gene);  // (0, 1]
-      const float u2 = rng_u01f(kb, 2 * (uint64_t)gene + 1);
+    // one 64-bit draw decides both individuals' indpb hits (32 bits each),
+    // one more feeds the shared Box-Muller pair (24 bits per uniform)
+    const uint64_t hb = splitmix64(k5 ^ (uint64_t)gene);
+    const bool h0 = mut0 && (double)(uint32_t)hb * 0x1.0p-32 < a.indpb;
+    const bool h1 = mut1 && (double)(uint32_t)(hb >> 32) * 0x1.0p-32 < a.indpb;
+    if (h0 || h1) {
+      const uint64_t nb = splitmix64(k6 ^ (uint64_t)gene);
+      const float u1 = 1.0f - (float)(nb >> 40) * 0x1.0p-24f;  // (0, 1]
+      const float u2 = (float)((nb >> 8) & 0xFFFFFFu) * 0x1.0p-24f;
       const float r = sqrtf(-2.0f * logf(u1));
       float sn, cs;
       sincosf(6.2831853f * u2, &sn, &cs);
-      if (hit[0]) x1 = __dadd_rn(x1, __dadd_rn(a.mu, __dmul_rn(a.sigma, (double)(r * cs))));
-      if (hit[1]) x2 = __dadd_rn(x2, __dadd_rn(a.mu, __dmul_rn(a.sigma, (double)(r * sn))));
+      if (h0) x1 = __dadd_rn(x1, __dadd_rn(a.mu, __dmul_rn(a.sigma, (double)(r * cs))));
+      if (h1) x2 = __dadd_rn(x2, __dadd_rn(a.mu, __dmul_rn(a.sigma, (double)(r * sn))));
     }
-    off[(long)i0 * a.stride + gene] = (WT)x1;
-    if (has1) off[(long)i1 * a.stride + gene] = (WT)x2;
-    if (gene == 0) {
-      a.invalid[i0] = (uint8_t)(cx || mut[0]);
-      if (has1) a.invalid[i1] = (uint8_t)(cx || mut[1]);
-    }
+    o1[gene] = (WT)x1;
+    if (has1) o2[gene] = (WT)x2;
+  };
+  for (long g0 = 0; g0 < a.genes; g0 += 128) {
+    const long ga = g0 + lane, gb = g0 + 64 + lane;
+    const bool va = ga < a.genes, vb = gb < a.genes;
+    const double a1 = va ? (double)p1[ga] : 0.0, a2 = va && has1 ? (double)p2[ga] : 0.0;
+    const double b1 = vb ? (double)p1[gb] : 0.0, b2 = vb && has1 ? (double)p2[gb] : 0.0;
+    if (va) one(ga, a1, a2);
+    if (vb) one(gb, b1, b2);
+  }
+  if (lane == 0) {
+    a.invalid[i0] = (uint8_t)(cx || mut0);
+    if (has1) a.invalid[i1] = (uint8_t)(cx || mut1);
   }
 }
 
@@ -1912,7 +1925,7 @@ int32_t pg_ga_vary(const pg_ga_args *a, void *stream) {
     return fail(PG_ERR_INVALID, "varAnd: bad sizes or NULL buffers");
   if (a->n == 0) return PG_OK;
   const int pairs = (a->n + 1) / 2;
-  dim3 grid((unsigned)((a->genes + 255) / 256), (unsigned)(pairs < 65535 ? pairs : 65535));
+  const dim3 grid((unsigned)((pairs + 3) / 4));  // one wave per pair
   if (a->dtype == PG_F64)
     hipLaunchKernelGGL(k_vary<double>, grid, dim3(256), 0, (hipStream_t)stream, *a);
   else
