@@ -358,10 +358,22 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           const unsigned rbits = mask & ((1u << NG) - 1);
           for (int g0 = 0; g0 < n_nets; g0 += cap) {
             const int gn = min(cap, n_nets - g0);
-            for (int i = t; i < gn * per_net; i += kWideThreads) {
-              const int slot = i / per_net, net = cf[3 + g0 + slot];
-              const WT *v = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n + W2n;
-              w3s[i] = v[i - slot * per_net];
+            // kW3Batch loads in flight per thread before any LDS store (a
+            // load-then-store loop waits out one HBM round trip per element)
+            constexpr int kW3Batch = 8;
+            for (int i0 = t; i0 < gn * per_net; i0 += kW3Batch * kWideThreads) {
+              WT val[kW3Batch];
+#pragma unroll
+              for (int q = 0; q < kW3Batch; ++q) {
+                const int i = i0 + q * kWideThreads;
+                const int ii = i < gn * per_net ? i : i0;
+                const int slot = ii / per_net, net = cf[3 + g0 + slot];
+                const WT *v = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n + W2n;
+                val[q] = v[ii - slot * per_net];
+              }
+#pragma unroll
+              for (int q = 0; q < kW3Batch; ++q)
+                if (i0 + q * kWideThreads < gn * per_net) w3s[i0 + q * kWideThreads] = val[q];
             }
             __syncthreads();
             const int nchain = __builtin_popcount(mask) * O;
