@@ -259,9 +259,21 @@ class DeviceGA:
         self.hof_n = int(m)
         self._hof_fit_host = new_fit
 
-    def _record(self, g: int, nevals: int) -> dict:
-        f = self.fitness
-        vals = torch.stack([f.mean(), f.std(unbiased=False), f.min(), f.max()]).tolist()
+    @staticmethod
+    def _summary(fit: torch.Tensor, invalid: torch.Tensor):
+        """One device->host sync for the generation's host-side needs: whether
+        any fitness is NaN, the logbook statistics and nevals."""
+        v = torch.stack([torch.isnan(fit).any().double(), fit.mean(), fit.std(unbiased=False), fit.min(), fit.max(),
+                         invalid.sum().double()]).tolist()
+        if v[0]:
+            # a NaN fitness is a game whose calculate_reward divided by zero (utils.py:106-108)
+            raise ZeroDivisionError("float division by zero (calculate_reward with total_frames == 0)")
+        return v[1:5], int(v[5])
+
+    def _record(self, g: int, nevals: int, vals=None) -> dict:
+        if vals is None:
+            f = self.fitness
+            vals = torch.stack([f.mean(), f.std(unbiased=False), f.min(), f.max()]).tolist()
         rec = {"gen": g, "nevals": nevals, **dict(zip(STAT_FIELDS, vals))}
         self.logbook.append(rec)
         return rec
@@ -292,7 +304,7 @@ class DeviceGA:
         fit = self._evaluate(g, off)
         new_fit = torch.where(inv, fit, inherited)
         self._mark("evaluate")
-        self._check(new_fit)
+        stats, nevals = self._summary(new_fit, inv)
         # generation g + 1's parents are this offspring; its offspring go to
         # store[H:] (this generation's parents, free now), the buffer the swap
         # below makes next step's spare[H:]
@@ -301,7 +313,7 @@ class DeviceGA:
         self.fitness = new_fit
         self.store, self.spare = self.spare, self.store
         self.generation = g
-        rec = self._record(g, int(inv.sum()))
+        rec = self._record(g, nevals, stats)
         self._mark("record")
         return rec
 
