@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out/s12
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py > gpurun_out/s12/parity.log 2>&1 || exit 1
+timeout -k 10 400 python -u tools/sweep.py --libs neuro-genetic-pong-self-play_amd/libpong_ga.so,variants/lib_regcnt.so,neuro-genetic-pong-self-play_amd/libpong_ga.so,variants/lib_regcnt.so --lanes 8 --reps 5 > gpurun_out/s12/sweep.log 2>&1 || exit 1
+for v in default regcnt; do
+  if [ $v = default ]; then L=$PWD/neuro-genetic-pong-self-play_amd/libpong_ga.so; else L=$PWD/variants/lib_$v.so; fi
+  PONG_GA_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/s12/bench_$v.json 2> gpurun_out/s12/bench_$v.err || exit 1
+done
