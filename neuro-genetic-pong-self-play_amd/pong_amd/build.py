@@ -14,10 +14,11 @@ SOURCES = [os.path.join(CSRC, f) for f in ("pong_ga.hip", "pg_wide.hip", "pg_pix
 DEPS = SOURCES + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp")] + [
     os.path.join(REPO_DIR, "include", "pong_ga.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-# per-source flags: the ILP-maximising machine scheduler makes k_service's frame
-# loop 3 % faster on the bench (profiles/r01: 13.85 vs 14.3 ms per launch;
-# iterative-minreg +9 %, the newer RP trackers +6 %, -O2 +3 % slower)
-SOURCE_FLAGS = {"pong_ga.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# per-source flags: the iterative ILP machine scheduler makes k_service's frame
+# loop ~5 % faster on the bench than the default (13.57 vs 14.3 ms per launch;
+# max-ilp 13.85; iterative-minreg +9 %, max-memory-clause +4 %,
+# iterative-maxocc +37 %, the newer RP trackers +6 %, -O2 +3 % slower)
+SOURCE_FLAGS = {"pong_ga.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 ARCH = os.environ.get("PG_OFFLOAD_ARCH", "gfx950")
 
 

@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/neuro-genetic-pong-self-play_amd/csrc
 mkdir -p $ROOT/variants
 # the main build's machine scheduler for pong_ga.hip (pong_amd/build.py SOURCE_FLAGS); PG_SCHED overrides
-SCHED=${PG_SCHED:-max-ilp}
+SCHED=${PG_SCHED:-iterative-ilp}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -Wall \
   -Wno-unused-function -I $ROOT/include -mllvm -amdgpu-sched-strategy=$SCHED "$@" -c -o /tmp/pg_variant_$NAME.o \
   $C/pong_ga.hip
