@@ -234,7 +234,9 @@ def main():
                                          "same command (profiles/r01/pmc_traffic.json, separate --pmc passes); "
                                          "genome rows are re-read per game, the unique set is ~0.42 GB",
                          "engine": "compute-bound on the f32 vector ALU (v_pk_fma_f32, v_exp_f32, v_rcp_f32); "
-                                   "peak = MI355X f32 dense peak, identical for VALU and MFMA (157.3 TF)",
+                                   "peak = MI355X f32 dense peak, identical for VALU and MFMA (157.3 TF); the "
+                                   "kernel is VALU-issue-bound: 46 VALU instructions per env-step of which the "
+                                   "network's FMAs are 9, ~69 % issue utilisation (profiles/r01/pmc_sq_k_service.txt)",
                          "kernel": "k_service<8,16,3,double> (pg_eval_population: 8 games per wave, "
                                    "4 lanes per network, f64 service wave per block)",
                          "kernel_ms_per_launch": kernel_ms_mean,
