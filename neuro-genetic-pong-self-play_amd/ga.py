@@ -10,7 +10,6 @@ Changes from the reference:
 """
 import glob
 import os
-import pickle
 import random
 
 try:  # the real DEAP when present
@@ -19,6 +18,7 @@ except ImportError:  # offline: DEAP's algorithms restated in-repo
     from pong_amd.deap_compat import base, creator, tools
 
 from config import *  # noqa: F401,F403
+from pong_amd import deap_pickle
 from pong_amd.batched import batched_map
 from utils import calculate_gene_size
 
@@ -33,11 +33,13 @@ def _register_individual():
 def load_population_from_file(checkpoint):
     """Unpickle a save_checkpoint file (utils.py:116-125): population sorted by
     fitness (best first); restores ``random``'s state, the hall of fame and
-    NETWORK_SHAPE as module globals, like ga.py:41-53."""
+    NETWORK_SHAPE as module globals, like ga.py:41-53.  A file the reference
+    wrote names ``deap.creator.*`` / ``deap.tools.support.HallOfFame``; without
+    deap installed those resolve to the restatement (pong_amd.deap_pickle)."""
     global hall_of_fame, NETWORK_SHAPE
     print("Loading: {}".format(checkpoint))
     with open(checkpoint, "rb") as cp_file:
-        cp = pickle.load(cp_file)
+        cp = deap_pickle.load(cp_file)
     ranked = sorted(cp["population"], key=lambda ind: ind.fitness.values[0], reverse=True)
     random.setstate(cp["rndstate"])
     hall_of_fame = cp.get("hall_of_fame", hall_of_fame)

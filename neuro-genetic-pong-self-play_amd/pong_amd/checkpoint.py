@@ -13,19 +13,23 @@ Two formats:
   ``{population: [Individual], hall_of_fame: HallOfFame, rndstate:
   random.getstate(), network_shape}``, which ga.load_population_from_file
   (ga.py:41-53) resumes from; ``export_reference`` / ``import_reference``
-  convert between the two.
+  convert between the two.  Classes are pickled and resolved by DEAP's module
+  paths in both directions (``deap_pickle``), so the reference reads the
+  build's exports and the build reads the reference's checkpoints whether or
+  not deap is installed.
 """
 from __future__ import annotations
 
 import datetime
 import json
 import os
-import pickle
 import random
 import struct
 
 import numpy as np
 import torch
+
+from . import deap_pickle
 
 FORMAT = "pong_amd.device_ga/1"
 _DT = {torch.float64: "F64", torch.float32: "F32", torch.int64: "I64", torch.int32: "I32", torch.uint8: "U8"}
@@ -160,7 +164,7 @@ def export_reference(state, path: str = None) -> str:
         stamp = datetime.datetime.now().strftime("%H_%M_%S")
         path = os.path.join("checkpoints", "checkpoints", f"c_{stamp}.pkl")
     with open(path, "wb") as fh:
-        pickle.dump(payload, fh)
+        deap_pickle.dump(payload, fh)  # DEAP's class paths, readable by the reference's ga.py
     return path
 
 
@@ -169,9 +173,8 @@ def read_reference(path: str) -> dict:
     the reference on this machine (never a file shipped inside the reference):
     population genes/fitness/valid, hall-of-fame genes/fitness (best first),
     network_shape."""
-    _deap()  # the pickle's classes must be importable
     with open(path, "rb") as fh:
-        cp = pickle.load(fh)
+        cp = deap_pickle.load(fh)
     pop = cp["population"]
     genes = np.array([list(ind) for ind in pop], dtype=np.float64)
     valid = np.array([ind.fitness.valid for ind in pop], dtype=bool)
