@@ -24,6 +24,8 @@
  *                                utils.py:71-77, calculate_timeout_and_frames
  *                                main.py:128-135, calculate_reward utils.py:104-109
  * pg_forward                     NeuralNetwork.run numpy_nn.py:120-137 (batched)
+ * pg_decide                      get_actions' model.run argmax (main.py:143-150) as the
+ *                                hot kernel decides it (test / fixture entry point)
  * pg_physics_reset/pg_physics_step  env.reset()/env.step(action) main.py:56,77
  *                                (the build's SoA Pong; the emulator is absent)
  * pg_ga_select_tournament        tools.selTournament (ga.py:94; DEAP)
@@ -51,7 +53,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 3
+#define PG_ABI_VERSION 4
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -126,7 +128,8 @@ typedef struct pg_eval_args {
                                     certified f64 rules, [6] failures decided in-wave by the f32 plateau
                                     rule; wide kernel: [7] network weight passes; split and wide
                                     kernels: [8] episode frames not simulated because the rally was
-                                    periodic (frames = [0] + [8]); [9..11] 0 */
+                                    periodic (frames = [0] + [8]); [9] hard decisions (see hard_log);
+                                    [10..11] 0 */
   uint8_t *trace;                /* optional [trace_games, trace_cap] per-frame action codes */
   int32_t trace_games;           /* games (genome-major index g = i*n_games + game) traced */
   int32_t trace_cap;
@@ -134,6 +137,15 @@ typedef struct pg_eval_args {
   int32_t group_lanes;           /* lanes per game of RESIDENT (4..64) / SPLIT (8..64), 0 = auto */
   void *workspace;               /* device scratch of pg_eval_workspace_bytes() bytes */
   size_t workspace_bytes;
+  uint32_t *hard_log;            /* optional [hard_cap][8] records of the decisions no bound settles
+                                    (fixtures for tests/golden/nn_hard_cases): split kernel, forwards its
+                                    service wave hands to the numpy-order f64 forward; wide kernel,
+                                    decisions whose two largest activations lie within 1e-12 (not both
+                                    1.0).  Record: {row, flags, k0..k5}; flags bit 0 = row of the
+                                    opponents (else genomes), bits 8..15 the decided index, bits 16..23
+                                    the source (0 split, 1 wide).  counters[9] counts every such
+                                    decision, also past hard_cap (requires counters). */
+  int32_t hard_cap;
 } pg_eval_args;
 
 /* Trace byte: right_code | left_code << 2 | ball_visible << 4, where a code is
@@ -151,7 +163,29 @@ typedef struct pg_forward_args {
   int32_t *index;                /* [n] np.argmax of the output activations */
   double *act;                   /* optional [n, nodes[last]] output activations */
   uint64_t *counters;            /* optional [4]: [2] += passes re-decided in f64 (others unused) */
+  double *z_all;                 /* optional, PG_PREC_F64 only: [n, sum(nodes[1:])] every layer's
+                                    pre-activations np.dot(w, column) (numpy_nn.py:127), layer by layer */
+  double *h_all;                 /* optional, PG_PREC_F64 only: the same layout, the activations */
 } pg_forward_args;
+
+/* The split kernel's decision for given inputs: pass i is network row
+ * genome_index[i] (i if NULL) on the doubled-centroid features k[i][0..5]
+ * (utils.inference's inputs are k / 320; main.py:143-150).  It runs the very
+ * cascade k_service runs in a game -- the f32 pass and its certificate, the
+ * in-wave plateau rule, the service wave's plateau and certified f64 rules,
+ * and last the numpy-order f64 forward -- so fixtures of hard inputs pin the
+ * hot kernel's decisions.  [6, H <= 256, 2..4] networks. */
+typedef struct pg_decide_args {
+  pg_net net;
+  int32_t n;
+  const void *genomes;           /* [*, genome_stride] (net.dtype) */
+  int64_t genome_stride;
+  const int32_t *genome_index;   /* [n] or NULL */
+  const int32_t *k;              /* [n, 6] doubled centroids, each in [0, 320] */
+  int32_t *index;                /* out [n] np.argmax of NeuralNetwork.run's activations */
+  int32_t *stage;                /* optional out [n]: 0 f32 certificate, 1 in-wave plateau rule,
+                                    2 service wave's certified rules, 3 numpy-order f64 forward */
+} pg_decide_args;
 
 /* Struct-of-arrays game state: int32 [PG_STATE_FIELDS, n], field f of game i
  * at state[f * n + i]; 64 bytes per game. */
@@ -253,6 +287,7 @@ int32_t pg_gene_count(const pg_net *net);
 
 int32_t pg_eval_population(const pg_eval_args *args, void *stream);
 int32_t pg_forward(const pg_forward_args *args, void *stream);
+int32_t pg_decide(const pg_decide_args *args, void *stream);
 int32_t pg_physics_reset(int32_t *state, int32_t n, const uint64_t *seeds,
                          const int32_t *one_player, void *stream);
 /* actions [n]: bit0 right up, bit1 right down, bit2 left up, bit3 left down */

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pg_f64math.h"
+
 namespace pg {
 
 // ---- playfield geometry: the 160x160 crop (rows 34..193) of obs.npy ----
@@ -244,9 +246,92 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // numpy's sigmoid 1 / (1 + np.e ** -x) (numpy_nn.py:22-23) in f64; np.e is the
-// double nearest e.  Plain IEEE ops in this order; pow is the only libm call.
-__device__ __forceinline__ double sigmoid_f64(double z) {
-  return 1.0 / __dadd_rn(1.0, pow(2.718281828459045, -z));
+// double nearest e; pow(e_d, -x) correctly rounded (pg_f64math.h).
+__device__ __forceinline__ double sigmoid_f64(double z) { return pg_sigmoid_f64(z); }
+
+// ------------------------------------------------ numpy's np.dot order ----
+// Row j of np.dot(W, x) for a C-contiguous [n, m] float64 W (numpy_nn.py:127):
+// numpy calls cblas_dgemv, OpenBLAS runs dgemv_t, whose x86-64 AVX2/FMA kernel
+// (dgemv_t_4.c) takes the outputs 4 at a time, then 2, then 1 -- each with its
+// own summation -- over blocks of <= 2048 elements, then the m & 3 tail.  The
+// oracle restates the same order (or_blas_dot, pinned to np.dot by
+// tests/test_blas_order.py); kinds:
+//   0  j < 4 (n / 4):         s[i % 4] = fma(a_i, x_i, s[i % 4]); (s0 + s2) + (s1 + s3)
+//   1  the next 2 if n & 2:   s[i % 2] += a_i x_i (product rounded);  s0 + s1
+//   2  the last if n & 1:     s[i % 4] += a_i x_i;                    (s0 + s2) + (s1 + s3)
+__host__ __device__ constexpr int blas_kind(int j, int n) {
+  return j < 4 * (n >> 2) ? 0 : (((n & 2) && j < 4 * (n >> 2) + 2) ? 1 : 2);
+}
+
+// One block's partial sums (nb a multiple of 4) starting at element i0.
+template <class AF, class XF>
+__device__ __forceinline__ double blas_block(AF a, XF x, int i0, int nb, int kind) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (kind == 0) {
+#pragma unroll 2
+    for (int i = i0; i < i0 + nb; i += 4) {
+      s0 = fma(a(i), x(i), s0);
+      s1 = fma(a(i + 1), x(i + 1), s1);
+      s2 = fma(a(i + 2), x(i + 2), s2);
+      s3 = fma(a(i + 3), x(i + 3), s3);
+    }
+    return __dadd_rn(__dadd_rn(s0, s2), __dadd_rn(s1, s3));
+  }
+  if (kind == 1) {
+#pragma unroll 2
+    for (int i = i0; i < i0 + nb; i += 2) {
+      s0 = __dadd_rn(s0, __dmul_rn(a(i), x(i)));
+      s1 = __dadd_rn(s1, __dmul_rn(a(i + 1), x(i + 1)));
+    }
+    return __dadd_rn(s0, s1);
+  }
+#pragma unroll 2
+  for (int i = i0; i < i0 + nb; i += 4) {
+    s0 = __dadd_rn(s0, __dmul_rn(a(i), x(i)));
+    s1 = __dadd_rn(s1, __dmul_rn(a(i + 1), x(i + 1)));
+    s2 = __dadd_rn(s2, __dmul_rn(a(i + 2), x(i + 2)));
+    s3 = __dadd_rn(s3, __dmul_rn(a(i + 3), x(i + 3)));
+  }
+  return __dadd_rn(__dadd_rn(s0, s2), __dadd_rn(s1, s3));
+}
+
+// The m & 3 trailing elements at i0 added to y (dgemv_t_4.c's tail, as GCC
+// contracts it): 1: fma(a, x, y); 2: y + fma(a0, x0, a1 x1);
+// 3: y + fma(a2, x2, fma(a0, x0, a1 x1)).
+template <class AF, class XF>
+__device__ __forceinline__ double blas_tail(AF a, XF x, int i0, int m3, double y) {
+  if (m3 == 1) return fma(a(i0), x(i0), y);
+  if (m3 == 0) return y;
+  const double t = fma(a(i0), x(i0), __dmul_rn(a(i0 + 1), x(i0 + 1)));
+  return __dadd_rn(y, m3 == 2 ? t : fma(a(i0 + 2), x(i0 + 2), t));
+}
+
+// A hidden unit of the game networks: np.dot over [x0..x5] (+ the bias weight
+// times 1.0 when b).  m = 6 or 7: one 4-element block -- the same
+// (p0 + p2) + (p1 + p3) for every kind -- then the 2- or 3-element tail.
+__device__ __forceinline__ double blas_dot6(const double w[7], const double x[6], int b) {
+  const double blk = __dadd_rn(__dadd_rn(__dmul_rn(w[0], x[0]), __dmul_rn(w[2], x[2])),
+                               __dadd_rn(__dmul_rn(w[1], x[1]), __dmul_rn(w[3], x[3])));
+  const double t = fma(w[4], x[4], __dmul_rn(w[5], x[5]));
+  return __dadd_rn(blk, b ? fma(w[6], 1.0, t) : t);
+}
+
+// y_j = np.dot(W, x)[j], a(i) = W[j][i], x(i) = x[i], i < m.
+template <class AF, class XF>
+__device__ __forceinline__ double blas_dot(AF a, XF x, int m, int kind) {
+  const int m3 = m & 3, m2 = (m & 2047) - m3;
+  int m1 = m & ~3, nb = 2048, i0 = 0;
+  double y = 0.0;
+  while (nb == 2048) {
+    m1 -= nb;
+    if (m1 < 0) {
+      if (m2 == 0) break;
+      nb = m2;
+    }
+    y = __dadd_rn(y, blas_block(a, x, i0, nb, kind));
+    i0 += nb;
+  }
+  return blas_tail(a, x, i0, m3, y);
 }
 
 }  // namespace pg

@@ -36,6 +36,8 @@ struct EvalParams {
   int32_t *status_game;  // [n*games] scratch: zero-division per game
   uint64_t *counters;
   uint8_t *trace;
+  uint32_t *hard_log;    // optional [hard_cap][8] (pg_eval_args.hard_log)
+  int hard_cap;
   unsigned int *work;    // dynamic game counter (workspace)
   int64_t gstride, ostride;
   uint64_t seed;
@@ -78,6 +80,17 @@ __device__ inline double feat64_flip(int k) { return (160.0 - __dmul_rn(0.5, (do
 
 
 int num_cus();
+
+// Append one hard-decision record (pg_eval_args.hard_log); counters[9] counts them all.
+__device__ inline void log_hard(const EvalParams &p, int row, int is_opp, int idx, int source, const int k[6]) {
+  if (!p.hard_log || !p.counters) return;
+  const unsigned long long r = atomicAdd((unsigned long long *)&p.counters[9], 1ull);
+  if (r >= (unsigned long long)p.hard_cap) return;
+  uint32_t *rec = p.hard_log + r * 8;
+  rec[0] = (uint32_t)row;
+  rec[1] = (uint32_t)(is_opp & 1) | ((uint32_t)(idx & 255) << 8) | ((uint32_t)(source & 255) << 16);
+  for (int i = 0; i < 6; ++i) rec[2 + i] = (uint32_t)k[i];
+}
 
 // [6, H1, H2, O] networks (two hidden layers, H1, H2 <= 512, O in 2..4,
 // n_games <= 8) on the weight-streaming kernel k_wide (pg_wide.hip).

@@ -13,12 +13,12 @@
 //   B  layer 1, thread j = hidden unit j, every needed column.
 //   C  layer 2: W2 tiles of 512 rows x K columns (128 B per row) pass
 //      HBM -> registers -> LDS (two tiles in flight per block), thread t owns
-//      row t and accumulates its dot product in k order; the genome's tile
-//      serves its six games' columns.
+//      row t and accumulates its dot product in np.dot's order (four partial
+//      sums k mod 4, blas_dot); the genome's tile serves its six games' columns.
 //   D  layer 3: one thread per (column, output).
 //   E  wave 0: argmax, clamp, bookkeeping, termination, results.
-// Every dot product is numpy_nn's own operation sequence (numpy_nn.py:126-129:
-// W . [h; 1], a sequential f64 sum of f64 products, bias last) with the same
+// Every dot product is np.dot's own operation sequence (numpy_nn.py:126-129:
+// W . [h; 1] through OpenBLAS dgemv_t, pg_device.hpp blas_dot) with the same
 // sigmoid as k_general, so k_wide and k_general agree bit for bit; the
 // streamed weights are exact (f32 or f64 genomes, widened to f64).
 #include <hip/hip_runtime.h>
@@ -67,6 +67,22 @@ __device__ __forceinline__ int argmax_np(const double *v, int O) {
   for (int j = 1; j < O && !__builtin_isnan(v[best]); ++j)
     if (__builtin_isnan(v[j]) || v[j] > v[best]) best = j;
   return best;
+}
+
+// A decision no bound settles (pg_eval_args.hard_log): the two largest
+// activations within 1e-12 of each other, not both saturated at 1.0.
+__device__ __forceinline__ bool near_tie(const double *v, int O) {
+  double t1 = -1.0, t2 = -1.0;
+  for (int j = 0; j < O; ++j) {
+    const double x = v[j];
+    if (x > t1) { t2 = t1; t1 = x; } else if (x > t2) { t2 = x; }
+  }
+  return t1 - t2 <= 1e-12 && !(t2 == 1.0);
+}
+__device__ __noinline__ void log_wide(const EvalParams &p, int row, int is_opp, int idx, const double *x) {
+  int k[6];
+  for (int i = 0; i < 6; ++i) k[i] = (int)rint(x[i] * 320.0);  // the doubled centroids back from k/320
+  log_hard(p, row, is_opp, idx, 1, k);
 }
 
 // Diagnostic build (-DPG_WIDE_STAMPS): thread 0 adds the shader-clock cycles
@@ -197,9 +213,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             for (int c = 0; c < NG; ++c) {
               if (!((mask >> c) & 1)) continue;
               const double *x = feat + c * 8;
-              double z = 0.0;
-              for (int i = 0; i < C1; ++i) z = __dadd_rn(z, __dmul_rn(wv[i], x[i]));
-              h1[j * NC + c] = sigmoid_f64_call(z);
+              h1[j * NC + c] = sigmoid_f64_call(blas_dot6(wv, x, b));
             }
           }
 #pragma unroll
@@ -207,9 +221,10 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             if (!((mask >> (NG + c)) & 1)) continue;
             const WT *row = opponents + orow[c] + (long)j * C1;
             const double *x = feat + (NG + c) * 8;
-            double z = 0.0;
-            for (int i = 0; i < C1; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], x[i]));
-            h1[j * NC + NG + c] = sigmoid_f64_call(z);
+            double wo[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) wo[i] = (i < C1) ? (double)row[i] : 0.0;
+            h1[j * NC + NG + c] = sigmoid_f64_call(blas_dot6(wo, x, b));
           }
         }
         if (b && t < NC) h1[H1 * NC + t] = 1.0;
@@ -222,11 +237,25 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
         // wave-instruction reads 8 rows x 128 B.  Tiles pass through a ring
         // of kDepth register sets: while tile s is multiplied out of LDS,
         // tiles s+1 .. s+kDepth are in flight.
-        double zg[NG];   // the genome's row sums (one per game)
-        double zop[NG];  // finished opponents' row sums (written once per network pass)
+        // Row sums in np.dot's order (pg_device.hpp blas_dot; C2 <= 513 is one
+        // block): four partial sums k mod 4 over k < m2 (kind 0: fused
+        // multiply-add; kind 1: two sums k mod 2; kind 2: rounded products),
+        // the m3 = C2 & 3 trailing weights kept for the tail after the last tile.
+        const int kind2 = blas_kind(t, H2);
+        const int m3 = C2 & 3, m2 = C2 - m3;
+        double zg[NG][4];  // the genome's partial sums (per game)
+        double zp[4];      // the current opponent network's partial sums
+        double zop[NG];    // finished opponents' row sums (written once per network pass)
+        double tw[3] = {0.0, 0.0, 0.0};  // the current network's tail weights
+        double tg[3] = {0.0, 0.0, 0.0};  // the genome's tail weights
 #pragma unroll
-        for (int c = 0; c < NG; ++c) { zg[c] = 0.0; zop[c] = 0.0; }
-        double zo = 0.0;  // the current opponent network's row sum
+        for (int c = 0; c < NG; ++c) {
+          zop[c] = 0.0;
+#pragma unroll
+          for (int l = 0; l < 4; ++l) zg[c][l] = 0.0;
+        }
+#pragma unroll
+        for (int l = 0; l < 4; ++l) zp[l] = 0.0;
         const int S = n_nets * T;
         const int lane_off = (t >> 3) * C2 * (int)sizeof(WT) + (t & 7) * 16;
         const int w2_bytes = H2 * C2 * (int)sizeof(WT);
@@ -261,6 +290,19 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           for (int it = 0; it < 8; ++it)
             *(uint4 *)((unsigned char *)tile + (it * 64 + (t >> 3)) * kTilePitch + (t & 7) * 16) = r[it];
         };
+        // one weight wk at row position kk (kk % 4 == l) into partial sums a
+        auto accum = [&](double (&a)[4], int l, double wk, double h) {
+          if (kind2 == 0) {
+            a[l] = fma(wk, h, a[l]);
+          } else {
+            const double pr = __dmul_rn(wk, h);
+            if (kind2 == 1) {
+              if (l & 1) a[1] = __dadd_rn(a[1], pr); else a[0] = __dadd_rn(a[0], pr);
+            } else {
+              a[l] = __dadd_rn(a[l], pr);
+            }
+          }
+        };
         // multiply tile s (in LDS) into the row sums and load tile sn into r
         auto compute = [&](int s, uint4 (&r)[8], int sn) {
           const Src src = source(sn);
@@ -275,29 +317,70 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           }
           const int net = cf[3 + s / T], tl = s % T, k0 = tl * K;
           const int kn = min(K, C2 - k0);
+          const bool full = k0 + K <= m2;  // the whole tile is inside the block (no tail, no end)
           const unsigned char *tr = (const unsigned char *)tile + t * kTilePitch;
           constexpr int E = 16 / (int)sizeof(WT);  // weights per 16-B piece
           if (net == 0) {
+            if (full && kind2 == 0) {  // the hot case: every element a fused multiply-add
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const uint4 v = *(const uint4 *)(tr + q * 16);
-              r[q] = load(src, q);
-              WT wq[E];
-              __builtin_memcpy(wq, &v, 16);
+              for (int q = 0; q < 8; ++q) {
+                const uint4 v = *(const uint4 *)(tr + q * 16);
+                r[q] = load(src, q);
+                WT wq[E];
+                __builtin_memcpy(wq, &v, 16);
 #pragma unroll
-              for (int e = 0; e < E; ++e) {
-                const int k = q * E + e;
-                if (k < kn) {
+                for (int e = 0; e < E; ++e) {
+                  const int k = q * E + e;
                   const double wk = (double)wq[e];
                   const double *hp = h1 + (k0 + k) * NC;
 #pragma unroll
-                  for (int c = 0; c < NG; ++c) zg[c] = __dadd_rn(zg[c], __dmul_rn(wk, hp[c]));
+                  for (int c = 0; c < NG; ++c) zg[c][k & 3] = fma(wk, hp[c], zg[c][k & 3]);
+                }
+              }
+            } else {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const uint4 v = *(const uint4 *)(tr + q * 16);
+                r[q] = load(src, q);
+                WT wq[E];
+                __builtin_memcpy(wq, &v, 16);
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                  const int k = q * E + e, kk = k0 + k;
+                  if (k < kn) {
+                    const double wk = (double)wq[e];
+                    if (kk < m2) {
+                      const double *hp = h1 + kk * NC;
+#pragma unroll
+                      for (int c = 0; c < NG; ++c) accum(zg[c], k & 3, wk, hp[c]);
+                    } else {
+#pragma unroll
+                      for (int i = 0; i < 3; ++i) tg[i] = (kk - m2 == i) ? wk : tg[i];
+                    }
+                  }
                 }
               }
             }
           } else {
-            const double *hp = h1 + k0 * NC + NG + net - 1;
-            double acc = tl == 0 ? 0.0 : zo;
+            const double *hp = h1 + NG + net - 1;
+            if (tl == 0) {
+#pragma unroll
+              for (int l = 0; l < 4; ++l) zp[l] = 0.0;
+            }
+            if (full && kind2 == 0) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const uint4 v = *(const uint4 *)(tr + q * 16);
+                r[q] = load(src, q);
+                WT wq[E];
+                __builtin_memcpy(wq, &v, 16);
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                  const int k = q * E + e;
+                  zp[k & 3] = fma((double)wq[e], hp[(k0 + k) * NC], zp[k & 3]);
+                }
+              }
+            } else {
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
               const uint4 v = *(const uint4 *)(tr + q * 16);
@@ -306,12 +389,24 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
               __builtin_memcpy(wq, &v, 16);
 #pragma unroll
               for (int e = 0; e < E; ++e) {
-                const int k = q * E + e;
-                if (k < kn) acc = __dadd_rn(acc, __dmul_rn((double)wq[e], hp[k * NC]));
+                const int k = q * E + e, kk = k0 + k;
+                if (k < kn) {
+                  const double wk = (double)wq[e];
+                  if (kk < m2) {
+                    accum(zp, k & 3, wk, hp[kk * NC]);
+                  } else {
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) tw[i] = (kk - m2 == i) ? wk : tw[i];
+                  }
+                }
               }
             }
-            zo = acc;
-            if (tl == T - 1) zop[net - 1] = acc;  // once per network pass
+            }
+            if (tl == T - 1) {  // once per network pass: the block sum and the tail
+              const double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(zp[0], zp[2]), __dadd_rn(zp[1], zp[3])));
+              zop[net - 1] =
+                  blas_tail([&](int i) { return tw[i - m2]; }, [&](int i) { return hp[i * NC]; }, m2, m3, y);
+            }
           }
         };
 
@@ -337,9 +432,15 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
         }
         // every tile read is behind the last barrier: h2 may overwrite the tile
         if (t < H2) {
+          double zgf[NG];
+#pragma unroll
+          for (int c = 0; c < NG; ++c) {
+            const double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(zg[c][0], zg[c][2]), __dadd_rn(zg[c][1], zg[c][3])));
+            zgf[c] = blas_tail([&](int i) { return tg[i - m2]; }, [&](int i) { return h1[i * NC + c]; }, m2, m3, y);
+          }
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
-            const double zc = c < NG ? zg[c] : zop[c - NG];
+            const double zc = c < NG ? zgf[c] : zop[c - NG];
             h2[t * NC + c] = ((mask >> c) & 1) ? sigmoid_f64_call(zc) : 0.0;
           }
         }
@@ -384,9 +485,8 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
               if (pos >= g0 && pos < g0 + gn) {
                 const WT *v = w3s + (pos - g0) * per_net + o * C3;
                 const double *hp = h2 + c;
-                double zz = 0.0;
-#pragma unroll 8
-                for (int j = 0; j < C3; ++j) zz = __dadd_rn(zz, __dmul_rn((double)v[j], hp[j * NC]));
+                const double zz = blas_dot([&](int j) { return (double)v[j]; }, [&](int j) { return hp[j * NC]; },
+                                           C3, blas_kind(o, O));
                 outv[c * 4 + o] = sigmoid_f64_call(zz);
               }
             }
@@ -400,8 +500,14 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       if (wid == 0 && active) {
         int right = 0;
         if (vis) {
-          right = index_to_code(argmax_np(outv + lane * 4, O));
-          if (kind == kOppNN) left = index_to_code(argmax_np(outv + (NG + lane) * 4, O));
+          const int ir = argmax_np(outv + lane * 4, O);
+          right = index_to_code(ir);
+          if (p.hard_log && near_tie(outv + lane * 4, O)) log_wide(p, gi, 0, ir, feat + lane * 8);
+          if (kind == kOppNN) {
+            const int il = argmax_np(outv + (NG + lane) * 4, O);
+            left = index_to_code(il);
+            if (p.hard_log && near_tie(outv + (NG + lane) * 4, O)) log_wide(p, p.opp[w], 1, il, feat + (NG + lane) * 8);
+          }
           c_fwd += 1 + (kind == kOppNN ? 1 : 0);
         }
         act_l = clamp_action(lc2, left);

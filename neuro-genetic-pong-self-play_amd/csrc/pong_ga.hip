@@ -56,21 +56,29 @@ int32_t fail(int32_t code, const char *fmt, ...) {
 
 // ===================================================== general (f64) path ==
 // One forward pass of NeuralNetwork.run (numpy_nn.py:120-137) by one wave, in
-// f64 with numpy_nn's operation order per unit (sequential dot product over
-// [inputs..., 1]); cur holds the input vector (with the trailing 1 if bias).
-// Returns the argmax index; cur/nxt are LDS buffers of max_width + 1 doubles.
+// f64 with numpy's operation order per unit (np.dot's BLAS order over
+// [inputs..., 1], blas_dot); cur holds the input vector (with the trailing 1 if
+// bias).  Returns the argmax index; cur/nxt are LDS buffers of max_width + 1
+// doubles.  With z_all/h_all (pg_forward's diagnostics) every layer's
+// pre-activations and activations are stored there as well.
 template <typename WT>
 __device__ int forward_f64_wave(const WT *__restrict__ w, const int *nodes, int n_nodes, int b,
-                                double *&cur, double *&nxt, int lane) {
+                                double *&cur, double *&nxt, int lane, double *z_all = nullptr,
+                                double *h_all = nullptr) {
   long off = 0;
+  int zo = 0;
   for (int l = 0; l + 1 < n_nodes; ++l) {
     const int nin = nodes[l], nout = nodes[l + 1], cols = nin + b;
     for (int j = lane; j < nout; j += 64) {
       const WT *row = w + off + (long)j * cols;
-      double z = 0.0;
-      for (int i = 0; i < cols; ++i) z = __dadd_rn(z, __dmul_rn((double)row[i], cur[i]));
+      const double *cv = cur;
+      const double z = blas_dot([&](int i) { return (double)row[i]; }, [&](int i) { return cv[i]; }, cols,
+                                blas_kind(j, nout));
       nxt[j] = sigmoid_f64(z);
+      if (z_all) z_all[zo + j] = z;
+      if (h_all) h_all[zo + j] = nxt[j];
     }
+    zo += nout;
     if (b && lane == 0) nxt[nout] = 1.0;
     wave_lds_sync();
     off += (long)cols * nout;
@@ -431,21 +439,19 @@ __device__ __forceinline__ int certify(const float z[O], float e) {
 }
 
 // The f64 re-decision of one forward pass by the L lanes of a group, in
-// numpy_nn's order: each hidden unit a sequential dot product over
-// [x..., 1], each output a sequential sum of the products W2[o][j] * s_j.
-// The products are formed by all lanes in parallel (a product's rounding does
-// not depend on who computes it) and only the dependent additions run
-// serially, out of LDS -- no serial global loads.
-// LDS: lds[0, H) hidden activations, lds[H + o*(H+1) + j] products, then O
-// output activations; f64_lds_doubles(H, O) doubles in all.
+// numpy's order: every dot product as np.dot runs it (blas_dot: OpenBLAS
+// dgemv_t's summation), every sigmoid correctly rounded (pg_sigmoid_f64).
+// Hidden units are strided over the lanes; the output rows are staged in LDS
+// by all lanes (coalesced) and lane o < O sums output o out of LDS -- no
+// serial global loads.
+// LDS: lds[0, H) hidden activations, lds[H + o*(H+1) + j] output weights,
+// then O output activations (f64_out_offset); f64_lds_doubles(H, O) doubles.
 __host__ __device__ constexpr int f64_lds_doubles(int H, int O) { return H + O * (H + 1) + O + 1; }
+__host__ __device__ constexpr int f64_out_offset(int H, int O) { return H + O * (H + 1); }
 
 template <int L, int U, int O, typename WT>
-__device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H, int b, const int *k, double *lds,
+__device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H, int b, const double *x, double *lds,
                                               int lig) {
-  double x[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) x[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
   const int cols = 6 + b;
 #pragma unroll 1
   for (int j = lig; j < H; j += L) {
@@ -453,27 +459,21 @@ __device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H,
     double w[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) w[i] = (i < 6 || b) ? (double)row[i] : 0.0;
-    double z = 0.0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) z = __dadd_rn(z, __dmul_rn(w[i], x[i]));
-    if (b) z = __dadd_rn(z, w[6]);
-    lds[j] = pg_sigmoid_f64(z);
+    lds[j] = pg_sigmoid_f64(blas_dot6(w, x, b));
   }
-  wave_lds_sync();
-  double *prod = lds + H;
+  double *w2 = lds + H;
   const WT *v = g + (long)H * cols;
 #pragma unroll 1
   for (int t = lig; t < O * (H + b); t += L) {
     const int o = t / (H + b), j = t - o * (H + b);
-    const double wv = (double)v[(long)o * (H + b) + j];
-    prod[o * (H + 1) + j] = (j < H) ? __dmul_rn(wv, lds[j]) : wv;  // bias column times 1.0
+    w2[o * (H + 1) + j] = (double)v[(long)o * (H + b) + j];
   }
   wave_lds_sync();
-  double *out = prod + O * (H + 1);
+  double *out = lds + f64_out_offset(H, O);
   if (lig < O) {
-    const double *pr = prod + lig * (H + 1);
-    double z = 0.0;
-    for (int j = 0; j < H + b; ++j) z = __dadd_rn(z, pr[j]);
+    const double *wr = w2 + lig * (H + 1);
+    const double z = blas_dot([&](int j) { return wr[j]; }, [&](int j) { return j < H ? lds[j] : 1.0; }, H + b,
+                              blas_kind(lig, O));
     out[lig] = pg_sigmoid_f64(z);
   }
   wave_lds_sync();
@@ -482,6 +482,16 @@ __device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H,
     if (__builtin_isnan(out[o]) || out[o] > out[best]) best = o;
   wave_lds_sync();
   return best;
+}
+
+// The same from the doubled-centroid features k (utils.inference's values).
+template <int L, int U, int O, typename WT>
+__device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H, int b, const int *k, double *lds,
+                                              int lig) {
+  double x[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
+  return forward_f64_group<L, U, O, WT>(g, H, b, (const double *)x, lds, lig);
 }
 
 __device__ __forceinline__ float feat32(int k) { return (float)k * 0.003125f; }  // k / 320, <= 2u rel. error
@@ -969,8 +979,18 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           int idx = plateau_decide<O>(zf, slots[sl].e, lane64);
           if (idx < 0) idx = fast_f64_decide<O, WT>(g, H, b, k, lane64);
           // bit 8 / bit 9 of the answer: decided by the numpy-order forward / by the certified one
-          idx = idx < 0 ? (256 | forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64))
-                        : (512 | idx);
+          if (idx < 0) {
+            idx = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64);
+            if (p.hard_log && lane64 == 0) {
+              const long off = g - (const WT *)p.genomes;
+              const bool own = off >= 0 && off < (long)p.n_genomes * p.gstride;
+              log_hard(p, (int)(own ? off / p.gstride : (g - (const WT *)p.opponents) / p.ostride), own ? 0 : 1,
+                       idx, 0, k);
+            }
+            idx |= 256;
+          } else {
+            idx |= 512;
+          }
           if (lane64 == 0) {
             slots[sl].idx = idx;
             __threadfence_block();
@@ -1191,6 +1211,92 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   if (lane64 == 0) atomicAdd(&waves_done, 1);
 }
 
+// --------------------------------------------------------------- decide ----
+// k_service's decision cascade on given inputs (pg_decide): the split layout's
+// f32 pass (load_net_pk / partial_pk / group_sum<HL>, the same z and bound e a
+// game half-group computes), certify, the in-wave plateau rule, then the
+// service wave's plateau_decide, fast_f64_decide and numpy-order forward --
+// the same device functions, so a fixture of hard inputs pins the decisions
+// k_service makes on them.  One wave: 64 / HL passes' f32 parts in parallel,
+// then each failing pass through the wave-wide service cascade.
+struct DecideParams {
+  const void *genomes;
+  const int32_t *gidx;
+  const int32_t *k;
+  int32_t *index;
+  int32_t *stage;
+  int64_t gstride;
+  int n, H, b;
+};
+
+template <int HL, int U, int O, typename WT>
+__global__ __launch_bounds__(64) void k_decide(DecideParams p) {
+  constexpr int GPW = 64 / HL;
+  extern __shared__ double lds_dec[];  // f64_lds_doubles(H, O)
+  __shared__ float zs[GPW][4];
+  __shared__ float es[GPW];
+  __shared__ int res[GPW], stg[GPW];
+  const int lane = threadIdx.x, grp = lane / HL, hl = lane % HL;
+  const WT *genomes = (const WT *)p.genomes;
+  for (int base = blockIdx.x * GPW; base < p.n; base += gridDim.x * GPW) {
+    const int t = base + grp;
+    if (t < p.n) {
+      const WT *g = genomes + (long)(p.gidx ? p.gidx[t] : t) * p.gstride;
+      NetP<U, O> net;
+      load_net_pk<HL, U, O, WT>(net, g, p.H, p.b, hl);
+      int k[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) k[i] = p.k[(long)t * 6 + i];
+      float acc[O], z[O];
+      partial_pk<U, O>(net, k, acc);
+#pragma unroll
+      for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
+      int idx = certify<O>(z, net.e), st = 0;
+      if (idx < 0) {
+        idx = plateau_f32<O>(z, net.e);
+        st = 1;
+      }
+      if (hl == 0) {
+#pragma unroll
+        for (int o = 0; o < O; ++o) zs[grp][o] = z[o];
+        es[grp] = net.e;
+        res[grp] = idx;
+        stg[grp] = st;
+      }
+    }
+    wave_lds_sync();
+    for (int q = 0; q < GPW; ++q) {
+      const int t2 = base + q;
+      if (t2 >= p.n || res[q] >= 0) continue;  // wave-uniform
+      const WT *g = genomes + (long)(p.gidx ? p.gidx[t2] : t2) * p.gstride;
+      int k[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) k[i] = p.k[(long)t2 * 6 + i];
+      float zf[O];
+#pragma unroll
+      for (int o = 0; o < O; ++o) zf[o] = zs[q][o];
+      int idx = plateau_decide<O>(zf, es[q], lane);
+      int st = 2;
+      if (idx < 0) idx = fast_f64_decide<O, WT>(g, p.H, p.b, k, lane);
+      if (idx < 0) {
+        idx = forward_f64_group<64, 1, O, WT>(g, p.H, p.b, (const int *)k, lds_dec, lane);
+        st = 3;
+      }
+      wave_lds_sync();
+      if (lane == 0) {
+        res[q] = idx;
+        stg[q] = st;
+      }
+      wave_lds_sync();
+    }
+    if (hl == 0 && t < p.n) {
+      p.index[t] = res[grp];
+      if (p.stage) p.stage[t] = stg[grp];
+    }
+    wave_lds_sync();
+  }
+}
+
 // ------------------------------------------------------------- fitness ----
 // evaluate()'s return: sum(all_rewards) (left to right from int 0) / float(GAMES_TO_PLAY).
 __global__ void k_fitness(const double *rewards, const int32_t *status_game, int n, int games,
@@ -1214,11 +1320,12 @@ struct FwdParams {
   const double *x;
   int32_t *index;
   double *act;
+  double *z_all, *h_all;  // optional [n, sum(nodes[1:])]: every layer's pre-activations / activations
   uint64_t *counters;
   int64_t gstride;
   int n;
   int nodes[PG_MAX_NODES];
-  int n_nodes, bias, max_width;
+  int n_nodes, bias, max_width, n_units;
 };
 
 template <typename WT>
@@ -1234,7 +1341,9 @@ __global__ __launch_bounds__(64) void k_forward_general(FwdParams p) {
     for (int i = lane; i < n_in; i += 64) cur[i] = p.x[(long)t * n_in + i];
     if (p.bias && lane == 0) cur[n_in] = 1.0;
     wave_lds_sync();
-    const int idx = forward_f64_wave(gw, p.nodes, p.n_nodes, p.bias, cur, nxt, lane);
+    const int idx = forward_f64_wave(gw, p.nodes, p.n_nodes, p.bias, cur, nxt, lane,
+                                     p.z_all ? p.z_all + (long)t * p.n_units : nullptr,
+                                     p.h_all ? p.h_all + (long)t * p.n_units : nullptr);
     if (lane == 0) p.index[t] = idx;
     if (p.act)
       for (int j = lane; j < n_out; j += 64) p.act[(long)t * n_out + j] = cur[j];
@@ -1249,7 +1358,7 @@ __global__ __launch_bounds__(256) void k_forward_resident(FwdParams p) {
   extern __shared__ double lds_all[];
   const int lig = threadIdx.x & (L - 1);
   const int grp = threadIdx.x / L;
-  double *lds = lds_all + grp * (H + 1 + O + 1);
+  double *lds = lds_all + grp * f64_lds_doubles(H, O);
   uint32_t slow = 0;
   for (int t = blockIdx.x * GPB + grp; t < p.n; t += gridDim.x * GPB) {
     const long row = p.gidx ? p.gidx[t] : t;
@@ -1275,28 +1384,12 @@ __global__ __launch_bounds__(256) void k_forward_resident(FwdParams p) {
       if (!tight) idx = -1;
     }
     if (idx < 0) {
-      // arbitrary f64 inputs here: run the f64 pass on them directly
-      const int cols = 6 + b;
-      for (int j = lig; j < H; j += L) {
-        const WT *r = gw + (long)j * cols;
-        double zz = 0.0;
-        for (int i = 0; i < 6; ++i) zz = __dadd_rn(zz, __dmul_rn((double)r[i], p.x[(long)t * 6 + i]));
-        if (b) zz = __dadd_rn(zz, (double)r[6]);
-        lds[j] = sigmoid_f64(zz);
-      }
-      wave_lds_sync();
-      if (lig < O) {
-        const WT *v = gw + (long)H * cols + (long)lig * (H + b);
-        double zz = 0.0;
-        for (int j = 0; j < H; ++j) zz = __dadd_rn(zz, __dmul_rn((double)v[j], lds[j]));
-        if (b) zz = __dadd_rn(zz, (double)v[H]);
-        lds[H + 1 + lig] = sigmoid_f64(zz);
-      }
-      wave_lds_sync();
-      idx = 0;  // np.argmax: the first NaN if any, else the first maximum
-      for (int o = 1; o < O && !__builtin_isnan(lds[H + 1 + idx]); ++o)
-        if (__builtin_isnan(lds[H + 1 + o]) || lds[H + 1 + o] > lds[H + 1 + idx]) idx = o;
-      if (p.act && lig < O) p.act[(long)t * O + lig] = lds[H + 1 + lig];
+      // arbitrary f64 inputs here: the group's f64 pass on them directly
+      double xd[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) xd[i] = p.x[(long)t * 6 + i];
+      idx = forward_f64_group<L, U, O, WT>(gw, H, b, (const double *)xd, lds, lig);
+      if (p.act && lig < O) p.act[(long)t * O + lig] = lds[f64_out_offset(H, O) + lig];
       wave_lds_sync();
       slow += (lig == 0);
     } else if (p.act && lig < O) {
@@ -1669,7 +1762,7 @@ static int32_t launch_resident_any(const EvalParams &p, ResidentChoice c, int O,
 template <int L, int U, int O, typename WT>
 static int32_t launch_fwd_resident(const FwdParams &p, hipStream_t s) {
   constexpr int GPB = 256 / L;
-  const size_t lds = (size_t)GPB * (p.nodes[1] + 1 + O + 1) * sizeof(double);
+  const size_t lds = (size_t)GPB * f64_lds_doubles(p.nodes[1], O) * sizeof(double);
   const int want = (p.n + GPB - 1) / GPB;
   const int cap = num_cus() * 8;
   const int grid = want < cap ? want : cap;
@@ -1769,6 +1862,8 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   p.trace = a->trace;
   p.trace_games = a->trace ? a->trace_games : 0;
   p.trace_cap = a->trace_cap;
+  p.hard_log = a->hard_cap > 0 ? a->hard_log : nullptr;
+  p.hard_cap = a->hard_cap;
   p.work = (unsigned int *)a->workspace;
   p.status_game = (int32_t *)((char *)a->workspace + 256);
   p.gstride = a->genome_stride;
@@ -1851,10 +1946,15 @@ int32_t pg_forward(const pg_forward_args *a, void *stream) {
   p.x = a->x;
   p.index = a->index;
   p.act = a->act;
+  p.z_all = a->z_all;
+  p.h_all = a->h_all;
   p.counters = a->counters;
   p.gstride = a->genome_stride;
   p.n = a->n;
   for (int i = 0; i < a->net.n_nodes; ++i) p.nodes[i] = a->net.nodes[i];
+  for (int i = 1; i < a->net.n_nodes; ++i) p.n_units += a->net.nodes[i];
+  if ((a->z_all || a->h_all) && a->precision != PG_PREC_F64)
+    return fail(PG_ERR_INVALID, "z_all/h_all need precision PG_PREC_F64");
   p.n_nodes = a->net.n_nodes;
   p.bias = a->net.bias ? 1 : 0;
   p.max_width = max_width(a->net);
@@ -1875,6 +1975,57 @@ int32_t pg_forward(const pg_forward_args *a, void *stream) {
     hipLaunchKernelGGL(k_forward_general<float>, dim3(grid), dim3(64), lds, s, p);
   PG_HIP(hipGetLastError());
   return PG_OK;
+}
+
+int32_t pg_decide(const pg_decide_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  int32_t rc = check_net(a->net, false);
+  if (rc != PG_OK) return rc;
+  if (!resident_shape_ok(a->net)) return fail(PG_ERR_UNSUPPORTED, "pg_decide: the split kernel's shapes only");
+  if (a->n < 0) return fail(PG_ERR_INVALID, "n=%d < 0", a->n);
+  if (a->n == 0) return PG_OK;
+  const int G = gene_count(a->net);
+  if (!a->genomes || a->genome_stride < G || !a->k || !a->index)
+    return fail(PG_ERR_INVALID, "genomes/k/index NULL or genome_stride < gene count %d", G);
+  DecideParams p;
+  memset(&p, 0, sizeof(p));
+  p.genomes = a->genomes;
+  p.gidx = a->genome_index;
+  p.k = a->k;
+  p.index = a->index;
+  p.stage = a->stage;
+  p.gstride = a->genome_stride;
+  p.n = a->n;
+  p.H = a->net.nodes[1];
+  p.b = a->net.bias ? 1 : 0;
+  const int H = p.H, O = a->net.nodes[2];
+  const int L = choose_split_lanes(H);
+  const size_t lds = (size_t)f64_lds_doubles(H, O) * sizeof(double);
+  const int cap = num_cus() * 8;
+  hipStream_t s = (hipStream_t)stream;
+  const bool f64 = a->net.dtype == PG_F64;
+#define PG_DEC(LL, UU)                                                                              \
+  if (L == LL && (LL / 2) * UU >= H) {                                                              \
+    constexpr int GPW = 64 / (LL / 2);                                                              \
+    const int want = (a->n + GPW - 1) / GPW;                                                        \
+    const int grid = want < cap ? want : cap;                                                       \
+    if (O == 2) {                                                                                   \
+      if (f64) hipLaunchKernelGGL((k_decide<LL / 2, UU, 2, double>), dim3(grid), dim3(64), lds, s, p); \
+      else hipLaunchKernelGGL((k_decide<LL / 2, UU, 2, float>), dim3(grid), dim3(64), lds, s, p);      \
+    } else if (O == 3) {                                                                            \
+      if (f64) hipLaunchKernelGGL((k_decide<LL / 2, UU, 3, double>), dim3(grid), dim3(64), lds, s, p); \
+      else hipLaunchKernelGGL((k_decide<LL / 2, UU, 3, float>), dim3(grid), dim3(64), lds, s, p);      \
+    } else {                                                                                        \
+      if (f64) hipLaunchKernelGGL((k_decide<LL / 2, UU, 4, double>), dim3(grid), dim3(64), lds, s, p); \
+      else hipLaunchKernelGGL((k_decide<LL / 2, UU, 4, float>), dim3(grid), dim3(64), lds, s, p);      \
+    }                                                                                               \
+    PG_HIP(hipGetLastError());                                                                      \
+    return PG_OK;                                                                                   \
+  }
+  // the layouts launch_service_any picks for choose_split_lanes(H)
+  PG_DEC(8, 1) PG_DEC(8, 2) PG_DEC(8, 4) PG_DEC(8, 8) PG_DEC(8, 16) PG_DEC(32, 8) PG_DEC(64, 8)
+#undef PG_DEC
+  return fail(PG_ERR_UNSUPPORTED, "pg_decide: no layout for H=%d", H);
 }
 
 int32_t pg_physics_reset(int32_t *state, int32_t n, const uint64_t *seeds, const int32_t *one_player,

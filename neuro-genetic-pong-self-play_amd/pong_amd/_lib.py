@@ -16,7 +16,7 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 3
+PG_ABI_VERSION = 4
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -52,6 +52,7 @@ class PgEvalArgs(ctypes.Structure):
         ("trace", _vp), ("trace_games", ctypes.c_int32), ("trace_cap", ctypes.c_int32),
         ("kernel", ctypes.c_int32), ("group_lanes", ctypes.c_int32),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+        ("hard_log", _vp), ("hard_cap", ctypes.c_int32),
     ]
 
 
@@ -59,7 +60,14 @@ class PgForwardArgs(ctypes.Structure):
     _fields_ = [
         ("net", PgNet), ("n", ctypes.c_int32), ("genomes", _vp), ("genome_stride", ctypes.c_int64),
         ("genome_index", _vp), ("x", _vp), ("precision", ctypes.c_int32), ("index", _vp),
-        ("act", _vp), ("counters", _vp),
+        ("act", _vp), ("counters", _vp), ("z_all", _vp), ("h_all", _vp),
+    ]
+
+
+class PgDecideArgs(ctypes.Structure):
+    _fields_ = [
+        ("net", PgNet), ("n", ctypes.c_int32), ("genomes", _vp), ("genome_stride", ctypes.c_int64),
+        ("genome_index", _vp), ("k", _vp), ("index", _vp), ("stage", _vp),
     ]
 
 
@@ -108,6 +116,7 @@ SIGNATURES = {
     "pg_gene_count": (ctypes.c_int32, [ctypes.POINTER(PgNet)]),
     "pg_eval_population": (ctypes.c_int32, [ctypes.POINTER(PgEvalArgs), _vp]),
     "pg_forward": (ctypes.c_int32, [ctypes.POINTER(PgForwardArgs), _vp]),
+    "pg_decide": (ctypes.c_int32, [ctypes.POINTER(PgDecideArgs), _vp]),
     "pg_physics_reset": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp, _vp]),
     "pg_physics_step": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp]),
     "pg_ga_select_tournament": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp]),

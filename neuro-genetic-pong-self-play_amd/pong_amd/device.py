@@ -103,11 +103,14 @@ class Evaluator:
     def evaluate(self, genomes: torch.Tensor, kind: torch.Tensor, opp: torch.Tensor, mult: torch.Tensor,
                  opponents: Optional[torch.Tensor] = None, trace_games: int = 0, trace_cap: int = 0,
                  out: Optional[EvalResult] = None, precision: Optional[str] = None,
-                 kernel: Optional[str] = None, group_lanes: Optional[int] = None, validate: bool = True):
+                 kernel: Optional[str] = None, group_lanes: Optional[int] = None, validate: bool = True,
+                 hard_log: Optional[torch.Tensor] = None):
         """Run every genome's games to termination; returns (EvalResult, trace or None).
 
         ``validate`` checks the schedule's opponent rows on the host first (one
         device sync); callers that built the schedule themselves may skip it.
+        ``hard_log`` ([cap, 8] int32, device) receives the decisions no bound
+        settles (pg_eval_args.hard_log); ``counters[9]`` counts them.
         """
         dev = self.device
         n = genomes.shape[0]
@@ -164,6 +167,11 @@ class Evaluator:
         a.counters = _ptr(out.counters)
         if trace is not None:
             a.trace, a.trace_games, a.trace_cap = _ptr(trace), trace_games, trace_cap
+        if hard_log is not None:
+            _need(hard_log, "hard_log", torch.int32, dev)
+            if hard_log.dim() != 2 or hard_log.shape[1] != 8:
+                raise ValueError("hard_log must be [cap, 8] int32")
+            a.hard_log, a.hard_cap = _ptr(hard_log), hard_log.shape[0]
         a.kernel = KERNELS[kernel or self.kernel]
         a.group_lanes = self.group_lanes if group_lanes is None else int(group_lanes)
         ws = self._workspace(a)
@@ -174,8 +182,13 @@ class Evaluator:
 
     # -------------------------------------------------------------- forward
     def forward(self, genomes: torch.Tensor, x: torch.Tensor, genome_index: Optional[torch.Tensor] = None,
-                precision: Optional[str] = None, want_act: bool = True):
-        """Batched NeuralNetwork.run: returns (argmax index [n] int32, activations [n, out] f64)."""
+                precision: Optional[str] = None, want_act: bool = True, want_layers: bool = False):
+        """Batched NeuralNetwork.run: returns (argmax index [n] int32, activations [n, out] f64).
+
+        ``want_layers`` (precision "f64" only) also stores every layer's
+        pre-activations and activations in ``self.last_layers`` = (z, h), each
+        [n, sum(nodes[1:])] f64.
+        """
         dev = self.device
         _need(genomes, "genomes", self.dtype, dev)
         n = x.shape[0]
@@ -196,10 +209,41 @@ class Evaluator:
         a.index = _ptr(index)
         a.act = _ptr(act)
         a.counters = _ptr(counters)
+        if want_layers:
+            units = sum(self.nodes[1:])
+            z_all = torch.empty((n, units), dtype=torch.float64, device=dev)
+            h_all = torch.empty((n, units), dtype=torch.float64, device=dev)
+            a.z_all, a.h_all = _ptr(z_all), _ptr(h_all)
+            self.last_layers = (z_all, h_all)
         with torch.cuda.device(dev):
             L.check("pg_forward", L.lib().pg_forward(ctypes.byref(a), _stream(dev)))
         self.last_forward_counters = counters
         return index, act
+
+    # --------------------------------------------------------------- decide
+    def decide(self, genomes: torch.Tensor, k: torch.Tensor, genome_index: Optional[torch.Tensor] = None):
+        """The split kernel's decision cascade (pg_decide) on doubled-centroid
+        features k [n, 6] int32: returns (argmax index [n] int32, stage [n] int32)."""
+        dev = self.device
+        _need(genomes, "genomes", self.dtype, dev)
+        n = k.shape[0]
+        _need(k, "k", torch.int32, dev, (n, 6))
+        if genome_index is not None:
+            _need(genome_index, "genome_index", torch.int32, dev, (n,))
+        index = torch.empty(n, dtype=torch.int32, device=dev)
+        stage = torch.empty(n, dtype=torch.int32, device=dev)
+        a = L.PgDecideArgs()
+        a.net = self.net
+        a.n = n
+        a.genomes = _ptr(genomes)
+        a.genome_stride = genomes.stride(0) if genomes.shape[0] > 1 else genomes.shape[1]
+        a.genome_index = _ptr(genome_index)
+        a.k = _ptr(k)
+        a.index = _ptr(index)
+        a.stage = _ptr(stage)
+        with torch.cuda.device(dev):
+            L.check("pg_decide", L.lib().pg_decide(ctypes.byref(a), _stream(dev)))
+        return index, stage
 
 
 class Physics:

@@ -84,6 +84,8 @@ class DeviceGA:
         self.profile = None      # dict: when set, step() adds per-phase wall ms (with device syncs)
         self._t_mark = self._t_sub = 0.0
         self._next = None        # (generation, inv, inherited): offspring already varied into spare[H:]
+        self.hard_log = None     # optional [cap, 8] int32: the evaluation's hard decisions (pg_eval_args.hard_log)
+        self.on_evaluate = None  # optional callable(g, rows, opponents, result), right after each evaluation
 
     # ------------------------------------------------------------ views
     @property
@@ -171,10 +173,12 @@ class DeviceGA:
         if self.eval_events is not None:
             self.eval_events[0].record()
         res, _ = self.ev.evaluate(rows[self.lo:self.hi], kind, opp, mult, opponents=opponents, out=out,
-                                  validate=False)
+                                  validate=False, hard_log=self.hard_log)
         if self.eval_events is not None:
             self.eval_events[1].record()
         self.last = res
+        if self.on_evaluate is not None:
+            self.on_evaluate(g, rows[self.lo:self.hi], opponents, res)
         return PD.gather_fitness(res.fitness, self.P, self.group) if self.world > 1 else res.fitness
 
     @staticmethod

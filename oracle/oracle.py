@@ -72,6 +72,8 @@ def lib() -> ctypes.CDLL:
         L.or_env_done.argtypes = [ctypes.POINTER(OrState)]
         L.or_gene_count.argtypes = [ctypes.POINTER(OrNet)]
         L.or_nn_run.argtypes = [dp, ctypes.POINTER(OrNet), dp, dp]
+        L.or_blas_gemv.argtypes = [dp, ctypes.c_int, ctypes.c_int, dp, dp]
+        L.or_blas_gemv.restype = None
         L.or_play_game.argtypes = [dp, ctypes.POINTER(OrNet), ctypes.c_int, dp, ctypes.c_double,
                                    ctypes.c_uint64, ctypes.POINTER(OrGameResult),
                                    ctypes.POINTER(ctypes.c_uint8), ctypes.c_int]
@@ -127,6 +129,17 @@ def nn_run(genes, nodes, x, bias=True):
     out = np.zeros(nodes[-1], dtype=np.float64)
     idx = lib().or_nn_run(_dp(g), net.ref, _dp(xx), _dp(out))
     return idx, out
+
+
+def blas_gemv(w, x):
+    """np.dot(w, x) restated in OpenBLAS dgemv_t's operation order (pong_oracle.c or_blas_dot)."""
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    xx = np.ascontiguousarray(x, dtype=np.float64)
+    n, m = w.shape
+    assert xx.shape == (m,)
+    y = np.zeros(n, dtype=np.float64)
+    lib().or_blas_gemv(_dp(w), n, m, _dp(xx), _dp(y))
+    return y
 
 
 class Env:

@@ -156,6 +156,72 @@ int or_gene_count(const or_net *net) {
   return total; /* utils.calculate_gene_size, utils.py:128-136 */
 }
 
+/* Row j of y = W @ x as numpy computes it (numpy_nn.py:127 np.dot(w, column)).
+ * numpy hands a C-contiguous float64 matrix times a vector to cblas_dgemv
+ * (RowMajor, NoTrans), which OpenBLAS runs as dgemv_t over the transposed view:
+ * each output is a dot product of length m, taken in blocks of at most 2048
+ * elements (the last block m2 = (m & 2047) - (m & 3), the m & 3 trailing
+ * elements after all blocks).  Within a block the kernel depends on the output's
+ * position among the n outputs (dgemv_t_4.c: 4 outputs at a time, then 2, then 1):
+ *   kind 0 (j < 4*(n/4)): 4 partial sums i mod 4, fused multiply-add,
+ *                         block = (s0 + s2) + (s1 + s3);
+ *   kind 1 (next 2 if n & 2): 2 partial sums i mod 2, product rounded then added,
+ *                         block = s0 + s1;
+ *   kind 2 (last if n & 1): 4 partial sums i mod 4, product rounded then added,
+ *                         block = (s0 + s2) + (s1 + s3);
+ * y accumulates the blocks (y + block); then the tail: 1 element y = fma(a, x, y);
+ * 2: y + fma(a0, x0, a1 x1); 3: y + fma(a2, x2, fma(a0, x0, a1 x1)).  That is the
+ * x86-64 AVX2/FMA kernel numpy's OpenBLAS (0.3.29, DYNAMIC_ARCH) selects on
+ * Haswell-class and later cores, checked against np.dot in tests/test_blas_order.py. */
+double or_blas_dot(const double *a, const double *x, int m, int j, int n) {
+  const int kind = j < 4 * (n >> 2) ? 0 : ((n & 2) && j < 4 * (n >> 2) + 2) ? 1 : 2;
+  const int m3 = m & 3, m2 = (m & 2047) - m3;
+  int m1 = m & ~3, nb = 2048, start = 0;
+  double y = 0.0;
+  while (nb == 2048) {
+    m1 -= nb;
+    if (m1 < 0) {
+      if (m2 == 0) break;
+      nb = m2;
+    }
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, blk;
+    const double *ab = a + start, *xb = x + start;
+    if (kind == 0) {
+      for (int i = 0; i < nb; ++i) s[i & 3] = fma(ab[i], xb[i], s[i & 3]);
+      blk = (s[0] + s[2]) + (s[1] + s[3]);
+    } else if (kind == 1) {
+      for (int i = 0; i < nb; ++i) {
+        const double p = ab[i] * xb[i];
+        s[i & 1] = s[i & 1] + p;
+      }
+      blk = s[0] + s[1];
+    } else {
+      for (int i = 0; i < nb; ++i) {
+        const double p = ab[i] * xb[i];
+        s[i & 3] = s[i & 3] + p;
+      }
+      blk = (s[0] + s[2]) + (s[1] + s[3]);
+    }
+    y = y + blk;
+    start += nb;
+  }
+  const double *at = a + start, *xt = x + start;
+  if (m3 == 1) {
+    y = fma(at[0], xt[0], y);
+  } else if (m3 == 2) {
+    const double p1 = at[1] * xt[1];
+    y = y + fma(at[0], xt[0], p1);
+  } else if (m3 == 3) {
+    const double p1 = at[1] * xt[1];
+    y = y + fma(at[2], xt[2], fma(at[0], xt[0], p1));
+  }
+  return y;
+}
+
+void or_blas_gemv(const double *w, int n, int m, const double *x, double *y) {
+  for (int j = 0; j < n; ++j) y[j] = or_blas_dot(w + (long)j * m, x, m, j, n);
+}
+
 int or_nn_run(const double *genes, const or_net *net, const double *x, double *out_act) {
   double buf0[OR_MAX_WIDTH + 1], buf1[OR_MAX_WIDTH + 1];
   double *cur = buf0, *nxt = buf1;
@@ -168,8 +234,7 @@ int or_nn_run(const double *genes, const or_net *net, const double *x, double *o
     const int nin = net->nodes[l], nout = net->nodes[l + 1], cols = nin + b;
     for (int j = 0; j < nout; ++j) {
       const double *w = genes + off + (long)j * cols; /* row-major (out, in+bias) numpy_nn.py:63 */
-      double z = 0.0;
-      for (int i = 0; i < cols; ++i) z += w[i] * cur[i];
+      const double z = or_blas_dot(w, cur, cols, j, nout); /* np.dot(w, column), numpy_nn.py:127 */
       nxt[j] = 1.0 / (1.0 + pow(M_E, -z)); /* 1 / (1 + np.e ** -x), numpy_nn.py:22-23 */
     }
     if (b) nxt[nout] = 1.0;

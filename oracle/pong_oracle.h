@@ -7,7 +7,8 @@
  *
  * It is a plain-C restatement of the reference's per-genome evaluation
  * (n00b001/neuro-genetic-pong-self-play):
- *   - NeuralNetwork.run            numpy_nn.py:120-137  (f64, sigmoid = 1/(1+e**-x) numpy_nn.py:22-23)
+ *   - NeuralNetwork.run            numpy_nn.py:120-137  (f64, sigmoid = 1/(1+e**-x) numpy_nn.py:22-23;
+ *                                  np.dot in OpenBLAS dgemv_t's order, or_blas_dot)
  *   - populate_weights layout      numpy_nn.py:52-69
  *   - inference features           utils.py:139-153
  *   - get_actions                  main.py:138-154
@@ -96,6 +97,10 @@ int or_env_done(const or_pong_state *s);
 int or_gene_count(const or_net *net);
 /* numpy_nn.NeuralNetwork.run: returns argmax index; writes the final-layer
  * activations (len nodes[last]) into out_act if non-NULL. */
+/* np.dot(W, x) for a C-contiguous [n, m] float64 W, in the operation order of
+ * numpy's OpenBLAS dgemv_t (x86-64 AVX2/FMA kernel); see pong_oracle.c. */
+double or_blas_dot(const double *a, const double *x, int m, int j, int n);
+void or_blas_gemv(const double *w, int n, int m, const double *x, double *y);
 int or_nn_run(const double *genes, const or_net *net, const double *x, double *out_act);
 
 /* One perform_episode.  genes: right-paddle genome; opp_genes: left genome for
