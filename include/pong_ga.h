@@ -146,6 +146,14 @@ typedef struct pg_eval_args {
                                     the source (0 split, 1 wide).  counters[9] counts every such
                                     decision, also past hard_cap (requires counters). */
   int32_t hard_cap;
+  const int32_t *genome_rows;    /* optional [n_genomes] device: game block i plays genomes row
+                                    genome_rows[i] (NULL: row i); results stay indexed by i.  Lets the
+                                    caller evaluate only eaSimple's invalid_ind (main.py:165-170)
+                                    without copying rows; every index must be a valid row. */
+  const int32_t *n_active;       /* optional device int32: only game blocks i < *n_active are played
+                                    (n_genomes is then an upper bound; results of blocks >= *n_active,
+                                    and their counters, are left untouched) -- a count computed on the
+                                    device needs no host round trip before the launch. */
 } pg_eval_args;
 
 /* Trace byte: right_code | left_code << 2 | ball_visible << 4, where a code is
@@ -247,6 +255,7 @@ typedef struct pg_schedule_args {
   int32_t *kind;                 /* out [n, n_games] device, pg_opp_kind */
   int32_t *opp;                  /* out [n, n_games] device */
   double *mult;                  /* out [n, n_games] device */
+  const int32_t *rows;           /* optional [n] device: global row of entry i (NULL: row_offset + i) */
 } pg_schedule_args;
 
 /* HallOfFame.update (DEAP) over host arrays.  Members are in HallOfFame.items

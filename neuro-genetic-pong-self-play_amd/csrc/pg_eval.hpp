@@ -25,7 +25,8 @@ int32_t fail(int32_t code, const char *fmt, ...);
 struct EvalParams {
   const void *genomes;
   const void *opponents;
-  const int32_t *rows;  // unused (reserved)
+  const int32_t *rows;  // optional [n_genomes]: block i of games plays genome row rows[i] (NULL: row i)
+  const int32_t *n_active;  // optional device count: only blocks i < min(*n_active, n_genomes) are played
   const int32_t *kind;
   const int32_t *opp;
   const double *mult;
@@ -41,11 +42,24 @@ struct EvalParams {
   unsigned int *work;    // dynamic game counter (workspace)
   int64_t gstride, ostride;
   uint64_t seed;
-  int n_genomes, n_games, total;
+  int n_genomes, n_games, total, n_opponents;
   int trace_games, trace_cap;
   int nodes[PG_MAX_NODES];
   int n_nodes, bias, max_width;
 };
+
+// Genome blocks / games this launch plays (pg_eval_args.n_active).
+__device__ inline int active_genomes(const EvalParams &p) {
+  if (!p.n_active) return p.n_genomes;
+  const int a = *p.n_active;
+  return a < 0 ? 0 : (a < p.n_genomes ? a : p.n_genomes);
+}
+__device__ inline int active_total(const EvalParams &p) {
+  return p.n_active ? active_genomes(p) * p.n_games : p.total;
+}
+
+// Genome row played by block i of games (pg_eval_args.genome_rows).
+__device__ inline int genome_row(const EvalParams &p, int i) { return p.rows ? p.rows[i] : i; }
 
 // Results of one finished game: perform_episode's return value and the
 // bookkeeping around it (main.py:108-112, utils.py:104-109).

@@ -131,13 +131,15 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   const WT *opponents = (const WT *)p.opponents;
   const int n_games = p.n_games;
   uint64_t c_steps = 0, c_fwd = 0, c_games = 0, c_streams = 0, c_skip = 0;
+  const int n_genomes_active = active_genomes(p);
 
   for (;;) {  // genomes, one per workgroup at a time
     if (t == 0) ctl[0] = (int)atomicAdd(p.work, 1u);
     __syncthreads();
     const int gi = ctl[0];
-    if (gi >= p.n_genomes) break;
-    const WT *gbase = genomes + (long)gi * p.gstride;
+    if (gi >= n_genomes_active) break;
+    const int grow = genome_row(p, gi);
+    const WT *gbase = genomes + (long)grow * p.gstride;
 
     // game state: wave 0, lane g < n_games
     Pong st;
@@ -502,7 +504,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
         if (vis) {
           const int ir = argmax_np(outv + lane * 4, O);
           right = index_to_code(ir);
-          if (p.hard_log && near_tie(outv + lane * 4, O)) log_wide(p, gi, 0, ir, feat + lane * 8);
+          if (p.hard_log && near_tie(outv + lane * 4, O)) log_wide(p, grow, 0, ir, feat + lane * 8);
           if (kind == kOppNN) {
             const int il = argmax_np(outv + (NG + lane) * 4, O);
             left = index_to_code(il);

@@ -102,14 +102,15 @@ __global__ __launch_bounds__(64) void k_general(EvalParams p) {
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
   uint64_t c_steps = 0, c_fwd = 0, c_games = 0;
+  const int games_total = active_total(p);
   for (;;) {
     int w = 0;
     if (lane == 0) w = (int)atomicAdd(p.work, 1u);
     w = __builtin_amdgcn_readfirstlane(w);
-    if (w >= p.total) break;
+    if (w >= games_total) break;
     const int i = w / p.n_games, g = w % p.n_games;
     const int kind = p.kind[w];
-    const WT *gr = genomes + (long)i * p.gstride;
+    const WT *gr = genomes + (long)genome_row(p, i) * p.gstride;
     const WT *gl = (kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
     Pong st;
     st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
@@ -413,6 +414,7 @@ __device__ __forceinline__ int certify(const float z[O], float e) {
   // unsaturated one); (b) with none possibly saturated, the f32 winner must
   // lead the runner-up by 2e plus the plateau width at its value.
   constexpr float kTlo = 36.7367f, kThi = 36.7369f;
+  constexpr float kLowZ = -708.0f;
   int sat_res = -2;  // -2: no output may be saturated
 #pragma unroll
   for (int o = O - 1; o >= 0; --o) {
@@ -430,7 +432,10 @@ __device__ __forceinline__ int certify(const float z[O], float e) {
     top1 = gt ? z[o] : top1;
   }
   const float tw = 8.8817842e-16f * (__expf(fminf(top1 + e, 40.f)) + 1.0f);
-  const int uns_res = (top1 - top2 > 2.f * e + tw) ? w : -1;
+  // the gap rule needs the winner's S(z) normal: below z = -1022 ln 2 it is
+  // subnormal (coarse steps), and 0.0 for every z < -709.78 (pow overflows),
+  // where all such outputs tie and the first wins -- the f64 path decides there
+  const int uns_res = (top1 - top2 > 2.f * e + tw && top1 - e > kLowZ) ? w : -1;
   float sum = 0.f;
 #pragma unroll
   for (int o = 0; o < O; ++o) sum += z[o];
@@ -573,6 +578,7 @@ __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
   uint32_t slow = 0, c_fwd = 0;
   uint64_t c_steps = 0, c_games = 0;
 
+  const int games_total = active_total(p);
   int w;
   {
     int ww = 0;
@@ -580,12 +586,12 @@ __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
     w = uniformize<L>(group_broadcast<L>(ww, leader));
   }
   bool fresh = true;
-  while (w < p.total) {
+  while (w < games_total) {
     if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
       const int i = w / p.n_games;
       const int g = w - i * p.n_games;
       kind = uniformize<L>(p.kind[w]);
-      gr = genomes + (long)i * p.gstride;
+      gr = genomes + (long)genome_row(p, i) * p.gstride;
       load_net<L, U, O, WT>(nr, gr, H, b, lig);
       if (kind == kOppNN) {
         gl = opponents + (long)p.opp[w] * p.ostride;
@@ -774,7 +780,7 @@ __device__ int plateau_decide(const float *z, float e, int lane) {
       amb = true;  // NaN: numpy's NaN rule, in the f64 path
     } else if (zz >= 22.2) {
       double t = pg_exp_f64(-zz);
-      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z), as pg_sigmoid_f64
+      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
       const double v = t * 4503599627370496.0;    // 2^52 p
       const double fr = v - floor(v);
       amb = fabs(fr - 0.5) < 1e-6;  // too close to a rounding boundary to call
@@ -898,7 +904,7 @@ __device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int
       amb = true;  // NaN: numpy's NaN rule, in the full path
     } else if (zz >= 22.2) {
       double t = pg_exp_f64(-zz);
-      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z), as pg_sigmoid_f64
+      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
       const double vv = t * 4503599627370496.0;   // 2^52 p
       amb = fabs(vv - floor(vv) - 0.5) < 1e-6;
       m = (int)rint(vv);
@@ -924,7 +930,8 @@ __device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int
       } else {  // S_w below the regime: a strict gap above the plateau width
         const double top = z[w] + e[w];
         const double tw = 8.881784197001252e-16 * (pg_exp_f64(fmin(top, 40.0)) + 1.0);
-        ok = ok && (z[w] - e[w] > z[o] + e[o] + tw);
+        // and S_w normal (z > -1022 ln 2; S = 0.0 for all z < -709.78, see certify)
+        ok = ok && (z[w] - e[w] > z[o] + e[o] + tw) && (z[w] - e[w] > -708.0);
       }
     }
     if (ok) return w;
@@ -982,9 +989,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           if (idx < 0) {
             idx = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64);
             if (p.hard_log && lane64 == 0) {
-              const long off = g - (const WT *)p.genomes;
-              const bool own = off >= 0 && off < (long)p.n_genomes * p.gstride;
-              log_hard(p, (int)(own ? off / p.gstride : (g - (const WT *)p.opponents) / p.ostride), own ? 0 : 1,
+              const long oo = g - (const WT *)p.opponents;
+              const bool opp = p.opponents != p.genomes && oo >= 0 && oo < (long)p.n_opponents * p.ostride;
+              log_hard(p, (int)(opp ? oo / p.ostride : (g - (const WT *)p.genomes) / p.gstride), opp ? 1 : 0,
                        idx, 0, k);
             }
             idx |= 256;
@@ -1024,6 +1031,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   const WT *gm = genomes;
   uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0;
 
+  const int games_total = active_total(p);
   int w;
   {
     int ww = 0;
@@ -1035,12 +1043,12 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   uint64_t t_start = 0;
   uint32_t g_fails = 0, g_slow = 0;
 #endif
-  while (w < p.total) {
+  while (w < games_total) {
     if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
       const int i = w / p.n_games;
       const int g = w - i * p.n_games;
       kind = p.kind[w];
-      const WT *gr = genomes + (long)i * p.gstride;
+      const WT *gr = genomes + (long)genome_row(p, i) * p.gstride;
       gm = (side && kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
       load_net_pk<HL, U, O, WT>(net, gm, H, b, hl);
       st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
@@ -1299,10 +1307,10 @@ __global__ __launch_bounds__(64) void k_decide(DecideParams p) {
 
 // ------------------------------------------------------------- fitness ----
 // evaluate()'s return: sum(all_rewards) (left to right from int 0) / float(GAMES_TO_PLAY).
-__global__ void k_fitness(const double *rewards, const int32_t *status_game, int n, int games,
-                          double *fitness, int32_t *status) {
+__global__ void k_fitness(const double *rewards, const int32_t *status_game, int n, const int32_t *n_active,
+                          int games, double *fitness, int32_t *status) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (n_active && i >= *n_active)) return;  // rows not played keep their contents
   double s = 0.0;
   int err = 0;
   for (int g = 0; g < games; ++g) {
@@ -1567,7 +1575,7 @@ __global__ void k_schedule(pg_schedule_args a) {
   if (w >= (long)a.n * a.n_games) return;
   const long i = w / a.n_games;
   const int g = (int)(w % a.n_games);
-  const long row = a.row_offset + i;
+  const long row = a.rows ? (long)a.rows[i] : a.row_offset + i;
   int kind = kOppHard, opp = 0;
   double mult = 1.0;
   if (a.mode == PG_SCHED_SELFPLAY) {
@@ -1868,6 +1876,9 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   p.status_game = (int32_t *)((char *)a->workspace + 256);
   p.gstride = a->genome_stride;
   p.ostride = a->opponent_stride;
+  p.n_opponents = a->opponents ? a->n_opponents : 0;
+  p.rows = a->genome_rows;
+  p.n_active = a->n_active;
   p.seed = a->seed;
   p.n_genomes = a->n_genomes;
   p.n_games = a->n_games;
@@ -1924,7 +1935,7 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     return fail(PG_ERR_INVALID, "kernel=%d", a->kernel);
   }
   hipLaunchKernelGGL(k_fitness, dim3((a->n_genomes + 255) / 256), dim3(256), 0, s, a->rewards,
-                     p.status_game, a->n_genomes, a->n_games, a->fitness, a->status);
+                     p.status_game, a->n_genomes, a->n_active, a->n_games, a->fitness, a->status);
   PG_HIP(hipGetLastError());
   return PG_OK;
 }

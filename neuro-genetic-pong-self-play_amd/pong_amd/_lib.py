@@ -52,7 +52,8 @@ class PgEvalArgs(ctypes.Structure):
         ("trace", _vp), ("trace_games", ctypes.c_int32), ("trace_cap", ctypes.c_int32),
         ("kernel", ctypes.c_int32), ("group_lanes", ctypes.c_int32),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
-        ("hard_log", _vp), ("hard_cap", ctypes.c_int32),
+        ("hard_log", _vp), ("hard_cap", ctypes.c_int32), ("genome_rows", _vp),
+        ("n_active", _vp),
     ]
 
 
@@ -94,7 +95,7 @@ class PgScheduleArgs(ctypes.Structure):
         ("mode", ctypes.c_int32), ("n", ctypes.c_int32), ("n_games", ctypes.c_int32),
         ("row_offset", ctypes.c_int64), ("n_hof", ctypes.c_int32), ("hof_fitness", _vp),
         ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64),
-        ("kind", _vp), ("opp", _vp), ("mult", _vp),
+        ("kind", _vp), ("opp", _vp), ("mult", _vp), ("rows", _vp),
     ]
 
 

@@ -104,16 +104,21 @@ class Evaluator:
                  opponents: Optional[torch.Tensor] = None, trace_games: int = 0, trace_cap: int = 0,
                  out: Optional[EvalResult] = None, precision: Optional[str] = None,
                  kernel: Optional[str] = None, group_lanes: Optional[int] = None, validate: bool = True,
-                 hard_log: Optional[torch.Tensor] = None):
+                 hard_log: Optional[torch.Tensor] = None, rows: Optional[torch.Tensor] = None,
+                 n_active: Optional[torch.Tensor] = None):
         """Run every genome's games to termination; returns (EvalResult, trace or None).
 
         ``validate`` checks the schedule's opponent rows on the host first (one
         device sync); callers that built the schedule themselves may skip it.
         ``hard_log`` ([cap, 8] int32, device) receives the decisions no bound
         settles (pg_eval_args.hard_log); ``counters[9]`` counts them.
+        ``rows`` ([n] int32, device): evaluate genomes rows ``rows[i]`` (results
+        indexed by i) -- eaSimple's ``invalid_ind`` without copying rows.
+        ``n_active`` ([1] int32, device): play only entries i < n_active[0]
+        (the others' results are left untouched).
         """
         dev = self.device
-        n = genomes.shape[0]
+        n = genomes.shape[0] if rows is None else rows.shape[0]
         games = self.n_games
         _need(genomes, "genomes", self.dtype, dev)
         if genomes.dim() != 2 or genomes.shape[1] < self.genes:
@@ -125,8 +130,12 @@ class Evaluator:
             _need(opponents, "opponents", self.dtype, dev)
             if opponents.dim() != 2 or opponents.shape[1] < self.genes:
                 raise ValueError(f"opponents must be [H, >= {self.genes}], got {tuple(opponents.shape)}")
+        if rows is not None:
+            _need(rows, "rows", torch.int32, dev, (n,))
         if validate and n:
             # one host sync: out-of-range rows would fault the GPU, so check before launching
+            if rows is not None and bool(((rows < 0) | (rows >= genomes.shape[0])).any()):
+                raise ValueError(f"rows must index the {genomes.shape[0]}-row genomes tensor")
             nn_games = kind == L.PG_OPP_NN
             if bool(((kind < 0) | (kind > L.PG_OPP_NN)).any()):
                 raise ValueError("kind values must be pg_opp_kind codes 0..3")
@@ -154,7 +163,11 @@ class Evaluator:
         a.n_genomes = n
         a.n_games = games
         a.genomes = _ptr(genomes)
-        a.genome_stride = genomes.stride(0) if n > 1 else genomes.shape[1]
+        a.genome_stride = genomes.stride(0) if genomes.shape[0] > 1 else genomes.shape[1]
+        a.genome_rows = _ptr(rows)
+        if n_active is not None:
+            _need(n_active, "n_active", torch.int32, dev, (1,))
+            a.n_active = _ptr(n_active)
         if opponents is not None and opponents.shape[0] > 0:
             a.opponents = _ptr(opponents)
             a.opponent_stride = opponents.stride(0) if opponents.shape[0] > 1 else opponents.shape[1]
@@ -324,8 +337,9 @@ SCHEDULES = {"reference": L.PG_SCHED_REFERENCE, "selfplay": L.PG_SCHED_SELFPLAY}
 
 
 def schedule(mode: str, n: int, n_games: int, row_offset: int, hof_fitness: Optional[torch.Tensor], n_hof: int,
-             seed: int, generation: int, device):
-    """pg_ga_schedule: (kind, opp, mult) [n, n_games] of evaluate()'s games on device."""
+             seed: int, generation: int, device, rows: Optional[torch.Tensor] = None):
+    """pg_ga_schedule: (kind, opp, mult) [n, n_games] of evaluate()'s games on device;
+    ``rows`` ([n] int32) gives entry i's global population row (default row_offset + i)."""
     dev = torch.device(device)
     kind = torch.empty((n, n_games), dtype=torch.int32, device=dev)
     opp = torch.empty((n, n_games), dtype=torch.int32, device=dev)
@@ -336,8 +350,10 @@ def schedule(mode: str, n: int, n_games: int, row_offset: int, hof_fitness: Opti
             raise ValueError(f"hof_fitness holds {hof_fitness.numel()} values, n_hof={n_hof}")
     elif n_hof and mode == "reference":
         raise ValueError("reference schedule with a hall of fame needs hof_fitness")
+    if rows is not None:
+        _need(rows, "rows", torch.int32, dev, (n,))
     a = L.PgScheduleArgs(SCHEDULES[mode], n, n_games, row_offset, n_hof, _ptr(hof_fitness), seed, generation,
-                         _ptr(kind), _ptr(opp), _ptr(mult))
+                         _ptr(kind), _ptr(opp), _ptr(mult), _ptr(rows))
     with torch.cuda.device(dev):
         L.check("pg_ga_schedule", L.lib().pg_ga_schedule(ctypes.byref(a), _stream(dev)))
     return kind, opp, mult

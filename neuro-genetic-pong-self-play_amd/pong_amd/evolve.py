@@ -21,9 +21,9 @@ the fitness vector is all-gathered once per generation -- the only collective.
 
 Differences from DEAP (DESIGN.md "GA"): random draws are counter-based
 (distribution parity, not Mersenne-Twister stream parity); ``similar`` is the
-equality of 64-bit gene hashes; unmodified offspring keep their parent's
-fitness as DEAP's clones do (the batched launch plays their games too and the
-result is discarded).
+equality of 64-bit gene hashes; only the invalid offspring are evaluated
+(``invalid_ind``): unmodified ones keep their parent's fitness as DEAP's
+clones do, and their games are not played.
 """
 from __future__ import annotations
 
@@ -80,6 +80,8 @@ class DeviceGA:
         self.generation = -1  # -1: the initial population is not evaluated yet
         self.logbook = []
         self.last = None       # EvalResult of the latest evaluation (this rank's rows)
+        self.last_rows = None  # their population rows (int32, invalid first), None: the shard rows[lo:hi]
+        self.last_count = None  # device int32 [1]: how many of last_rows were played (None: all)
         self.eval_events = None  # optional (start, end) HIP events recorded around the evaluation launch
         self.profile = None      # dict: when set, step() adds per-phase wall ms (with device syncs)
         self._t_mark = self._t_sub = 0.0
@@ -162,24 +164,48 @@ class DeviceGA:
         self._hof_fit_host = np.zeros(0, np.float64)
 
     # ------------------------------------------------------------ steps
-    def _evaluate(self, g: int, rows: torch.Tensor) -> torch.Tensor:
-        """Fitness of every row of ``rows`` ([P, G]): this rank plays its shard's
-        games, then the fitness vector is all-gathered."""
-        n = self.hi - self.lo
-        kind, opp, mult = D.schedule(self.schedule, n, self.n_games, self.lo, self.hof_fitness, self.hof_n,
-                                     self.seed, g, self.device)
+    def _evaluate(self, g: int, rows: torch.Tensor, inv: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Fitness of the rows of ``rows`` ([P, G]) that eaSimple evaluates:
+        those ``inv`` marks (``invalid_ind``, main.py:165-170; every row if
+        None; the others' entries are 0).  Rank r plays the invalid rows of its
+        shard ``shard_range(P, r, N)`` and the shards' fitness is all-gathered
+        -- the generation's one collective.  The shard's invalid rows are
+        compacted on the device and the launch reads their count from device
+        memory (pg_eval_args.n_active), so no host round trip precedes it."""
+        lo, hi = self.lo, self.hi
+        n = hi - lo
+        local = count = None
+        if inv is not None:
+            inv_s = inv[lo:hi]
+            c_inv = torch.cumsum(inv_s, 0, dtype=torch.int32)
+            count = c_inv[-1:] if n else torch.zeros(1, dtype=torch.int32, device=self.device)
+            c_val = torch.cumsum(~inv_s, 0, dtype=torch.int32)
+            dest = torch.where(inv_s, c_inv - 1, count + c_val - 1).long()
+            local = torch.empty(n, dtype=torch.int32, device=self.device)
+            local[dest] = torch.arange(lo, hi, dtype=torch.int32, device=self.device)  # invalid rows first
+        kind, opp, mult = D.schedule(self.schedule, n, self.n_games, lo, self.hof_fitness, self.hof_n,
+                                     self.seed, g, self.device, rows=local)
         opponents = self.store[: self.hof_n] if self.hof_n else None
         out = self.last if (self.last is not None and self.last.fitness.shape[0] == n) else None
         if self.eval_events is not None:
             self.eval_events[0].record()
-        res, _ = self.ev.evaluate(rows[self.lo:self.hi], kind, opp, mult, opponents=opponents, out=out,
-                                  validate=False, hard_log=self.hard_log)
+        if local is None:
+            res, _ = self.ev.evaluate(rows[lo:hi], kind, opp, mult, opponents=opponents, out=out, validate=False,
+                                      hard_log=self.hard_log)
+        else:
+            res, _ = self.ev.evaluate(rows, kind, opp, mult, opponents=opponents, out=out, validate=False,
+                                      hard_log=self.hard_log, rows=local, n_active=count)
         if self.eval_events is not None:
             self.eval_events[1].record()
-        self.last = res
+        self.last, self.last_rows, self.last_count = res, local, count
         if self.on_evaluate is not None:
-            self.on_evaluate(g, rows[self.lo:self.hi], opponents, res)
-        return PD.gather_fitness(res.fitness, self.P, self.group) if self.world > 1 else res.fitness
+            self.on_evaluate(g, rows if local is not None else rows[lo:hi], opponents, res)
+        fit = res.fitness
+        if local is not None:  # back to shard order; rows not played (clones) read 0
+            shard = torch.zeros(n, dtype=torch.float64, device=self.device)
+            shard[local.long() - lo] = fit
+            fit = torch.where(inv_s, shard, torch.zeros_like(shard))
+        return PD.gather_fitness(fit, self.P, self.group) if self.world > 1 else fit
 
     @staticmethod
     def _check(fit: torch.Tensor):
@@ -285,7 +311,7 @@ class DeviceGA:
     def step(self) -> dict:
         """One eaSimple generation (or, first, the initial evaluation); returns the logbook row."""
         if self.generation < 0:
-            fit = self._evaluate(0, self.population)
+            fit = self._evaluate(0, self.population, ~self.valid)
             nevals = int((~self.valid).sum())
             new_fit = torch.where(self.valid, self.fitness, fit)
             self._check(new_fit)
@@ -305,7 +331,7 @@ class DeviceGA:
             inv, inherited = self._select_vary(g, self.population, self.fitness, off)
         self._next = None
         self._mark("select_vary")
-        fit = self._evaluate(g, off)
+        fit = self._evaluate(g, off, inv)  # invalid_ind only: clones keep their parent's fitness
         new_fit = torch.where(inv, fit, inherited)
         self._mark("evaluate")
         stats, nevals = self._summary(new_fit, inv)

@@ -27,6 +27,8 @@ Shims (all documented in DESIGN.md "Oracle"):
     ``fitness.valid/values`` (deap is absent).
 
 Usage:  python tests/golden/make_golden.py   (takes a few minutes)
+        python tests/golden/make_golden.py hard_cases gpurun_out/.../hard_cases.npz
+        (nn_hard_cases.npz from a tools/harvest_hard.py run on the GPU)
 """
 from __future__ import annotations
 
@@ -467,7 +469,66 @@ def gen_evaluate():
         json.dump(cases, fh)
 
 
+def _initial_rows(seed, n, G, sigma, dtype):
+    """tools/harvest_hard.py initial_rows: the harvest's host-drawn generation-0 rows."""
+    return (np.random.default_rng(seed).standard_normal((n, G)) * sigma).astype(dtype)
+
+
+def gen_hard_cases(harvest_path, wide_keep=1500):
+    """nn_hard_cases.npz: the decisions no bound settles, harvested on the GPU
+    from the bench distribution (tools/harvest_hard.py), run through the REAL
+    NeuralNetwork.run (numpy_nn.py:120-137) on x = (k / 2) / 160 -- the
+    inference features of the doubled centroids k (utils.py:139-153)."""
+    h = dict(np.load(harvest_path))
+    out = {}
+    for label in ("split", "wide"):
+        if f"{label}__shape" not in h:
+            continue
+        shape = [int(v) for v in h[f"{label}__shape"]]
+        seed, P, H, G, is64 = (int(v) for v in h[f"{label}__meta"])
+        sigma = float(h[f"{label}__sigma"][0])
+        dt = np.float64 if is64 else np.float32
+        gen, is_opp, row = h[f"{label}__gen"], h[f"{label}__is_opp"], h[f"{label}__row"]
+        gidx, k, idx_dev = h[f"{label}__gidx"], h[f"{label}__k"], h[f"{label}__idx_device"]
+        sel = np.arange(len(gen))
+        if label == "wide" and len(sel) > wide_keep:
+            sel = np.sort(np.random.default_rng(5).choice(len(sel), wide_keep, replace=False))
+        pop = _initial_rows(seed, P, G, sigma, dt) if (gen[sel] == 0).any() else None
+        hof = _initial_rows(seed + 1, H, G, sigma, dt) if (gen[sel] == 0).any() else None
+        stored = h[f"{label}__genes"]
+        acts, idxs = [], []
+        nets = {}
+        for i in sel:
+            key = (int(gen[i]), int(is_opp[i]), int(row[i]), int(gidx[i]))
+            if key not in nets:
+                g = stored[gidx[i]] if gidx[i] >= 0 else (hof if is_opp[i] else pop)[row[i]]
+                nets[key] = ref_nn.NeuralNetwork(nodes=list(shape), weights=[float(v) for v in g], bias=True)
+            net = nets[key]
+            x = [float((int(v) / 2) / 160) for v in k[i]]
+            try:
+                net.run(x)
+            except Exception:
+                pass
+            a = np.array(net.list_of_transitional_arrays[-1][:-1], dtype=np.float64)
+            acts.append(a)
+            idxs.append(int(np.argmax(a)))
+            if len(nets) > 64:
+                nets.clear()
+        idxs = np.array(idxs, np.int32)
+        print(f"{label}: {len(sel)} cases, device == reference in {int((idxs == idx_dev[sel]).sum())}", flush=True)
+        out.update({f"{label}__shape": np.array(shape, np.int32), f"{label}__meta": h[f"{label}__meta"],
+                    f"{label}__sigma": h[f"{label}__sigma"], f"{label}__gen": gen[sel], f"{label}__is_opp": is_opp[sel],
+                    f"{label}__row": row[sel], f"{label}__gidx": gidx[sel], f"{label}__k": k[sel],
+                    f"{label}__idx_device": idx_dev[sel], f"{label}__genes": stored,
+                    f"{label}__total": h[f"{label}__total"], f"{label}__idx_ref": idxs,
+                    f"{label}__act_ref": np.array(acts)})
+    np.savez_compressed(os.path.join(HERE, "nn_hard_cases.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["hard_cases"]:  # python make_golden.py hard_cases <harvest.npz>
+        gen_hard_cases(sys.argv[2])
+        sys.exit(0)
     which = sys.argv[1:] or ["nn", "helpers", "centroids", "episodes", "evaluate"]
     if "nn" in which:
         gen_nn_forward()

@@ -109,10 +109,13 @@ def test_device_ga_hall_of_fame_and_evaluations(gpu, oracle, schedule, dtype):
         ref = oracle.eval_population(pop, shape, kind.cpu().numpy(), opp.cpu().numpy(), mult.cpu().numpy(),
                                      opponents=hof_rows if len(hof_rows) else None, n_threads=8)
         fit = ga.fitness.cpu().numpy()
-        evaluated = ga.last.fitness.cpu().numpy()
-        np.testing.assert_array_equal(evaluated, ref["fitness"])
-        changed = fit != evaluated
-        assert changed.sum() <= ga.P - rec["nevals"]  # only clones keep a parent's fitness
+        # only eaSimple's invalid_ind are played (main.py:165-170); clones keep a parent's fitness
+        m = ga.P if ga.last_count is None else int(ga.last_count[0])
+        evaluated = ga.last.fitness[:m].cpu().numpy()
+        rows_ev = np.arange(ga.P) if ga.last_rows is None else ga.last_rows[:m].cpu().numpy()
+        assert len(rows_ev) == rec["nevals"] and rec["nevals"] > 0
+        np.testing.assert_array_equal(evaluated, ref["fitness"][rows_ev])
+        np.testing.assert_array_equal(fit[rows_ev], evaluated)
         _replay_hof(creator.EvoInd, hof, ga, ga.population, ga.fitness)
         assert [i.fitness.values[0] for i in hof] == ga.hof_member_fitness.tolist()
         hh = D.row_hash(ga.hall_of_fame, ga.G).cpu().numpy()
