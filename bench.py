@@ -37,6 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
+PROFILE_ROUND = "r02"           # profiles/<round>/ holds the PMC passes of the committed build
 
 
 def parse():
@@ -54,7 +55,7 @@ def parse():
     p.add_argument("--kernel", default="auto")
     p.add_argument("--sigma", type=float, default=3.0)
     p.add_argument("--seed", type=int, default=1234)
-    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
     a = p.parse_args()
@@ -73,6 +74,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu_pool = None
+    if world == 1 and not args.no_cpu_baseline:
+        # the CPU baseline's worker processes are forked now, before anything touches the GPU
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import numpy_loop
+        cpu_pool = numpy_loop.make_pool(args.cpu_threads)
     # PG_DIST_BACKEND=gloo with more ranks than GPUs: a rehearsal of the N > 1
     # path on a one-GPU box (ranks share devices); the driver's runs use RCCL
     backend = os.environ.get("PG_DIST_BACKEND", "nccl")
@@ -189,8 +196,8 @@ def main():
         out = wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all,
                           passes_all, kernel_ms_mean, skip_all)
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline: rank 0 at N=1 only
-            out["cpu_baseline"] = cpu_baseline(args, shape, ga, chunk=8,
-                                              max_rows=256)
+            out["cpu_baseline"] = cpu_baseline(args, shape, ga, chunk=8, max_rows=256, pool=cpu_pool)
+            cpu_pool.close()
         print(json.dumps(out), flush=True)
     elif rank == 0:
         env_steps_per_s = steps_all / elapsed
@@ -227,30 +234,50 @@ def main():
                        "failures_decided_in_wave": cert_all[2] / max(cert_all[0], 1.0),
                        "failures_decided_by_service_f64_certificate": cert_all[1] / max(cert_all[0], 1.0),
                        "numpy_order_f64_forwards_per_forward": slow_all / max(fwd_all, 1.0)},
-            "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved_tflops / F32_VECTOR_PEAK_TFLOPS,
-                         "traffic": _pmc_traffic(),
-                         "traffic_note": "HBM-side bytes per launch, rocprofv3 FETCH_SIZE + WRITE_SIZE of the "
-                                         "same command (profiles/r01/pmc_traffic.json, separate --pmc passes); "
-                                         "genome rows are re-read per game, the unique set is ~0.42 GB",
-                         "engine": "compute-bound on the f32 vector ALU (v_pk_fma_f32, v_exp_f32, v_rcp_f32); "
-                                   "peak = MI355X f32 dense peak, identical for VALU and MFMA (157.3 TF); the "
-                                   "kernel is VALU-issue-bound: 46 VALU instructions per env-step of which the "
-                                   "network's FMAs are 9, ~69 % issue utilisation (profiles/r01/pmc_sq_k_service.txt)",
-                         "kernel": "k_service<8,16,3,double> (pg_eval_population: 8 games per wave, "
-                                   "4 lanes per network, f64 service wave per block)",
-                         "kernel_ms_per_launch": kernel_ms_mean,
-                         "flops_per_forward": flops_per_forward,
-                         "forwards_per_launch": fwd_per_launch,
-                         "streaming_equivalent_GBps": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9,
-                         "streaming_equivalent_frac_of_hbm": streaming_bytes / (kernel_ms_mean / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "roofline": _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_per_forward,
+                                           fwd_per_launch, steps_per_launch, streaming_bytes, n_local, H),
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline: rank 0 at N=1 only
-            out["cpu_baseline"] = cpu_baseline(args, shape, ga)
+            out["cpu_baseline"] = cpu_baseline(args, shape, ga, pool=cpu_pool)
+            cpu_pool.close()
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_per_forward, fwd_per_launch,
+                       steps_per_launch, streaming_bytes, n_local, H):
+    """Roofline of k_service: compute-bound on the f32 vector ALU (VALU issue);
+    HBM traffic from the committed PMC passes of the same build and command."""
+    wt = 8 if dtype == torch.float64 else 4
+    pmc, src = _pmc("pmc_traffic.json")
+    traffic = pmc.get("traffic_bytes") if pmc else None
+    unique = (n_local + H) * G * wt  # every genome row and hall-of-fame row once
+    kernel_s = kernel_ms_mean / 1e3
+    return {"bound": "valu", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": achieved_tflops / F32_VECTOR_PEAK_TFLOPS,
+            "traffic": traffic,
+            "hbm_GBps": traffic / kernel_s / 1e9 if traffic else None,
+            "hbm_frac_of_peak": traffic / kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
+            "unique_row_bytes_per_launch": unique,
+            "refetch_ratio": traffic / unique if traffic else None,
+            "traffic_note": "HBM-side bytes per launch (L2 memory-side requests, MALL hits included): rocprofv3 "
+                            "FETCH_SIZE + WRITE_SIZE of the same bench command, separate --pmc passes (%s); each "
+                            "game loads both networks, so genome rows are fetched ~refetch_ratio times; hbm_GBps = "
+                            "traffic / this run's kernel time" % src,
+            "engine": "compute-bound on the f32 vector ALU (v_pk_fma_f32, v_exp_f32, v_rcp_f32), no MFMA: every "
+                      "game has its own 64x7 and 3x64 matrices applied to one input column; peak = MI355X f32 dense "
+                      "peak (157.3 TF, equal for VALU and MFMA); the kernel is VALU-issue-bound: most VALU "
+                      "instructions per env-step are physics, features, certificate and bookkeeping, not the "
+                      "network's FMAs (DESIGN.md 4.1, profiles/%s/pmc_sq_k_service.txt)" % PROFILE_ROUND,
+            "kernel": "k_service<8,16,3,double> (pg_eval_population: 8 games per wave, 4 lanes per network, "
+                      "f64 service wave per block)",
+            "kernel_ms_per_launch": kernel_ms_mean,
+            "flops_per_forward": flops_per_forward,
+            "forwards_per_launch": fwd_per_launch,
+            "streaming_equivalent_GBps": streaming_bytes / kernel_s / 1e9,
+            "streaming_equivalent_frac_of_hbm": streaming_bytes / kernel_s / 1e9 / HBM_PEAK_GBS}
 
 
 def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all, passes_all,
@@ -302,12 +329,17 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
     }
 
 
-def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16):
-    """The CPU oracle (C restatement of the reference loop, f64 numpy_nn
-    arithmetic) on the same workload's first genomes (this rank's population
-    rows against the current hall of fame), on the host cores."""
+def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
+    """The reference's CPU path on the host cores: oracle/numpy_loop.py, the
+    reference's per-frame numpy loop restated (main.py:69-112, utils.find_stuff,
+    numpy_nn.NeuralNetwork.run; calibrated against the real reference in the
+    build container: profiles/r02/cpu_calibration.json), on the same workload's
+    first genomes and schedule, in a process pool and on one core.  The C
+    restatement (oracle/pong_oracle.c, OpenMP) is reported beside it as
+    ``c_port``."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
+    import numpy_loop as NL
     from pong_amd import device as D
     O.build()
     lo = ga.lo
@@ -321,26 +353,51 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16):
     rows = np.unique(o)
     opponents = hof[torch.as_tensor(rows, device=hof.device)].double().cpu().numpy()
     o = np.searchsorted(rows, o).astype(np.int32)
+    secs = args.cpu_baseline_seconds
+    workers = args.cpu_threads
+    # numpy loop on `workers` processes, then on one core (~secs and ~secs/2 of wall time)
+    np_rows = min(n, 64 * workers)
+    rate_p, steps_p, games_p, dt_p = NL.timed_rate(shape, genomes[:np_rows], k[:np_rows], o[:np_rows],
+                                                   m[:np_rows], opponents, secs, workers, pool)
+    rate_1, steps_1, games_1, dt_1 = NL.timed_rate(shape, genomes[:8], k[:8], o[:8], m[:8], opponents,
+                                                   secs / 2, 1)
+    # the C restatement with OpenMP
     steps, done = 0, 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_baseline_seconds and done + chunk <= genomes.shape[0]:
+    while time.perf_counter() - t0 < secs / 2 and done + chunk <= genomes.shape[0]:
         r = O.eval_population(genomes[done:done + chunk], shape, k[done:done + chunk], o[done:done + chunk],
-                              m[done:done + chunk], opponents=opponents, n_threads=args.cpu_threads)
+                              m[done:done + chunk], opponents=opponents, n_threads=workers)
         steps += int(r["frames"].sum())
         done += chunk
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": f"{done} genomes x {args.games} games of the same self-play workload "
-                      f"({steps} env-steps in {dt:.1f} s, OpenMP over {args.cpu_threads} host threads)",
+    return {"value": rate_p, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "sample": f"the reference's per-frame numpy loop (oracle/numpy_loop.py) on {workers} worker processes: "
+                      f"{games_p} whole games of the same workload's first genomes ({steps_p} env-steps in "
+                      f"{dt_p:.1f} s); {workers} = this box's CPU share per GPU",
+            "one_core": {"value": rate_1, "sample": f"{games_1} games, {steps_1} env-steps in {dt_1:.1f} s"},
+            "calibration": "numpy_loop runs 1.11x the reference's own rate on the same games, equal rewards "
+                           "(profiles/r02/cpu_calibration.json)",
+            "c_port": {"value": steps / dt if dt > 0 else None, "cores": workers,
+                       "sample": f"C restatement (oracle/pong_oracle.c, OpenMP over {workers} threads): "
+                                 f"{done} genomes x {args.games} games ({steps} env-steps in {dt:.1f} s)"},
             "cpu": _cpu_model()}
 
 
+def _pmc(name):
+    """The newest committed PMC summary of this name (profiles/<round>/), and its path."""
+    for rnd in (PROFILE_ROUND, "r01"):
+        path = os.path.join("profiles", rnd, name)
+        try:
+            with open(os.path.join(REPO, path)) as fh:
+                return json.load(fh), path
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
 def _pmc_traffic(name="pmc_traffic.json"):
-    try:
-        with open(os.path.join(REPO, "profiles", "r01", name)) as fh:
-            return json.load(fh)["traffic_bytes"]
-    except (OSError, ValueError, KeyError):
-        return None
+    pmc, _ = _pmc(name)
+    return pmc.get("traffic_bytes") if pmc else None
 
 
 def _cpu_model():

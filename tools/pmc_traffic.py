@@ -16,21 +16,27 @@ import sys
 
 
 def mean_counter(path, name, kernel="k_service"):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
-    return sum(vals) / len(vals), len(vals)
+    """(mean counter value, dispatches, mean dispatch duration in ns) of one PMC pass."""
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
+    vals = [float(r["Counter_Value"]) for r in rows]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+    return sum(vals) / len(vals), len(vals), sum(durs) / len(durs)
 
 
 def main():
     run, out = sys.argv[1], sys.argv[2]
     kernel = sys.argv[3] if len(sys.argv) > 3 else "k_service"
-    fetch, nf = mean_counter(f"{run}/pmc_FETCH_SIZE/pmc_counter_collection.csv", "FETCH_SIZE", kernel)
-    write, nw = mean_counter(f"{run}/pmc_WRITE_SIZE/pmc_counter_collection.csv", "WRITE_SIZE", kernel)
+    fetch, nf, df = mean_counter(f"{run}/pmc_FETCH_SIZE/pmc_counter_collection.csv", "FETCH_SIZE", kernel)
+    write, nw, dw = mean_counter(f"{run}/pmc_WRITE_SIZE/pmc_counter_collection.csv", "WRITE_SIZE", kernel)
     kib = 1024.0
+    traffic = (fetch + write) * kib
+    dur_s = (df + dw) / 2 / 1e9  # the passes' mean dispatch time (counters on)
     res = {"kernel": kernel, "dispatches": [nf, nw],
            "fetch_bytes_raw": fetch * kib, "write_bytes": write * kib,
-           "traffic_bytes": (fetch + write) * kib,
+           "traffic_bytes": traffic,
            "traffic_bytes_fetch_x2": (2 * fetch + write) * kib,
+           "dispatch_ms": dur_s * 1e3,
+           "hbm_GBps": traffic / dur_s / 1e9,
            "source": run}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
