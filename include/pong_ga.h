@@ -88,9 +88,13 @@ typedef enum pg_kernel {
   PG_KERNEL_RESIDENT = 2,  /* [6, H<=256, 2..4]: one lane group holds both paddles' weights */
   PG_KERNEL_SPLIT = 3      /* [6, H<=256, 2..4]: half a lane group per paddle's network, plus one
                               f64 service wave per 1024-thread block for re-decisions */,
-  PG_KERNEL_WIDE = 4       /* [6, H1<=512, H2<=512, 1..4], n_games <= 8: one 512-thread workgroup per
+  PG_KERNEL_WIDE = 4,      /* [6, H1<=512, H2<=512, 1..4], n_games <= 8: one 512-thread workgroup per
                               genome plays its games in lockstep and streams W2 from HBM each frame
                               (numpy_nn's f64 order; AUTO picks it for H1 or H2 >= 64) */
+  PG_KERNEL_STAGED = 5     /* [6, H<=256, 2..4]: SPLIT's network lanes, with each block's physics and
+                              bookkeeping run by one environment wave (one lane per game) between the
+                              network stages; needs the larger workspace pg_eval_workspace_bytes()
+                              reports for it */
 } pg_kernel;
 
 /* NETWORK_SHAPE (config.py:30-32) + BIAS (config.py:34) + genome storage type. */

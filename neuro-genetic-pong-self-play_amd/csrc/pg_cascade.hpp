@@ -1,0 +1,701 @@
+// pg_cascade.hpp -- the certified f32 forward of the game networks and its
+// decision cascade, shared by the evaluation kernels (k_resident, k_service in
+// pong_ga.hip; k_staged in pg_staged.hip) and pg_decide:
+//   load_net / load_net_pk   a lane's share of a [6, H, O] network in VGPRs
+//                            (numpy_nn.py:52-69 gene layout) + the f32 bound
+//   partial_f32 / partial_pk the hidden layer and lane-partial output sums
+//   certify                  argmax of numpy's f64 S(z) proven from f32 z +- e
+//   plateau_f32              the same near saturation, in-wave
+//   plateau_decide / fast_f64_decide / forward_f64_group
+//                            the service wave's f64 steps (numpy_nn.py:120-137)
+// DESIGN.md 4.1 "Certified argmax, as a cascade".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pg_device.hpp"
+#include "pg_eval.hpp"
+#include "pg_f64math.h"
+
+namespace pg {
+
+// ================================================== resident (fast) path ==
+#ifndef PG_SLOW_INLINE
+#define PG_SLOW_INLINE __forceinline__
+#endif
+// hidden units whose weight loads are in flight together in load_net
+#ifndef PG_LOAD_BATCH
+#define PG_LOAD_BATCH 2
+#endif
+// minimum waves per SIMD requested from the register allocator (0 = no request)
+#ifndef PG_RES_WAVES
+#define PG_RES_WAVES 0
+#endif
+#if PG_RES_WAVES > 0
+#define PG_RES_BOUNDS __launch_bounds__(256, PG_RES_WAVES)
+#else
+#define PG_RES_BOUNDS __launch_bounds__(256)
+#endif
+constexpr float kU = 5.9604644775390625e-8f;  // 2^-24, f32 unit roundoff
+
+template <int U, int O>
+struct Net {
+  float w1[U][7];  // hidden unit j = lane + L*u: 6 input weights + bias weight
+  float w2[U][O];  // output weights of that hidden unit
+  float c[O];      // output biases
+  float e;         // certified bound on |z_o(f32) - z_o(exact)|, max over outputs
+};
+
+// Loads the [6, H, O] genome's weights for this lane (numpy_nn.py:52-69
+// layout: layer l is a row-major (out, in + bias) block, bias column last) and
+// computes the error bound of the f32 output pre-activations:
+//   hidden a_j error  <= 11u R_j           (R_j = sum_i |W1_ji| incl. bias; |x_i| <= 1)
+//   sigmoid error     <= 2.75u R_j + 4.5u  (v_exp_f32/v_rcp_f32 ~1 ulp, slope <= 1/4)
+//   output z_o error  <= sum_j |W2_oj| (3u R_j + 5u) + 13u (sum_j |W2_oj| + |c_o|)
+// and keeps twice the largest over o (DESIGN.md "Certified argmax").
+template <int L, int U, int O, typename WT>
+__device__ __forceinline__ void load_net(Net<U, O> &n, const WT *__restrict__ g, int H, int b, int lig) {
+  const int cols = 6 + b;
+  const long off2 = (long)H * cols;
+  float acc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = lig + L * u;
+    const bool ok = j < H;
+    const int jj = ok ? j : 0;  // padding units load a valid row and are zeroed
+    // Issue the unit's loads unconditionally, then mask arithmetically: a
+    // select on a load is turned into a branch around it by the backend,
+    // which serialises every load behind its own s_waitcnt.
+    WT raw[7 + O];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) raw[i] = g[(long)jj * cols + ((i < 6 || b) ? i : 0)];
+#pragma unroll
+    for (int o = 0; o < O; ++o) raw[7 + o] = g[off2 + (long)o * (H + b) + jj];
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const float m = (ok && (i < 6 || b)) ? 1.f : 0.f;
+      n.w1[u][i] = (float)raw[i] * m;
+      r += fabsf(n.w1[u][i]);
+    }
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      n.w2[u][o] = (float)raw[7 + o] * (ok ? 1.f : 0.f);
+      acc[o] += fabsf(n.w2[u][o]) * (3.f * r + 18.f);
+    }
+    // bound the loads in flight (f64: 2 VGPRs each): this cold spot would
+    // otherwise set the register budget of the whole kernel
+    if ((u + 1) % PG_LOAD_BATCH == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+  WT rawc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) rawc[o] = g[off2 + (long)o * (H + b) + (b ? H : 0)];
+  float e = 0.f;
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    n.c[o] = (float)rawc[o] * (b ? 1.f : 0.f);
+    e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + 13.f * fabsf(n.c[o])));
+  }
+  n.e = e;
+}
+
+__device__ __forceinline__ float sigmoid_f32(float a) {
+  // 1 / (1 + e^-a) with v_exp_f32 (2^x) and v_rcp_f32, ~1 ulp each
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a * -1.4426950408889634f));
+}
+
+// Hidden layer and the lane-partial output sums of one network for this lane.
+template <int U, int O>
+__device__ __forceinline__ void partial_f32(const Net<U, O> &n, const float x[6], float acc[O]) {
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float a = n.w1[u][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a = fmaf(n.w1[u][i], x[i], a);
+    const float s = sigmoid_f32(a);
+#pragma unroll
+    for (int o = 0; o < O; ++o) acc[o] = fmaf(n.w2[u][o], s, acc[o]);
+  }
+}
+
+// ---- packed layout of the split kernel -------------------------------------
+// Units in pairs (u = 2p, 2p+1) as float2, so the hidden layer runs on
+// v_pk_fma_f32: one instruction advances two independent dot products, which
+// halves the issue count and the length of the dependent chain per frame.
+// W1 is stored pre-scaled by -log2(e) / 320 (feature columns; the features
+// then enter as the exact integers k) and -log2(e) (bias column), so the
+// pre-activation feeds v_exp_f32 directly: a' = -a log2 e.  Each stored
+// weight carries one more rounding (<= 2u relative in all), and the fma chain
+// over exact inputs stays within the 11u R_j hidden-error term of load_net.
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+template <int U, int O>
+struct NetP {
+  static constexpr int P = (U + 1) / 2;  // unit pairs
+  float2v w1[P][7];  // pre-scaled input weights (6 features + bias) of units 2p, 2p+1
+  float2v w2[P][O];  // output weights of the pair
+  float c[O];        // output biases
+  float e;           // certified bound, as Net::e
+};
+
+// Number of f32 roundings in one output sum of the packed forward: a chain of
+// P pk_fma per component, the .x + .y fold, the group tree, + c, and the
+// f32 rounding of W2 -- bounded by U + log2(HL) + 3 for every layout.
+template <int HL, int U>
+__host__ __device__ constexpr int out_roundings() {
+  return U + (HL >= 32 ? 5 : HL >= 16 ? 4 : HL >= 8 ? 3 : HL >= 4 ? 2 : HL >= 2 ? 1 : 0) + 3;
+}
+
+template <int L, int U, int O, typename WT>
+__device__ __forceinline__ void load_net_pk(NetP<U, O> &n, const WT *__restrict__ g, int H, int b, int lig) {
+  constexpr int P = NetP<U, O>::P;
+  constexpr float kScaleX = -1.4426950408889634f / 320.f;
+  constexpr float kScaleB = -1.4426950408889634f;
+  const int cols = 6 + b;
+  const long off2 = (long)H * cols;
+  float acc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = 2 * p + h;
+      const int j = lig + L * u;
+      const bool ok = u < U && j < H;
+      const int jj = ok ? j : 0;  // padding units load a valid row and are zeroed
+      WT raw[7 + O];  // unconditional loads, masked arithmetically (see load_net)
+#pragma unroll
+      for (int i = 0; i < 7; ++i) raw[i] = g[(long)jj * cols + ((i < 6 || b) ? i : 0)];
+#pragma unroll
+      for (int o = 0; o < O; ++o) raw[7 + o] = g[off2 + (long)o * (H + b) + jj];
+      float r = 0.f;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const float w = (float)raw[i] * ((ok && (i < 6 || b)) ? 1.f : 0.f);
+        r += fabsf(w);
+        n.w1[p][i][h] = w * (i < 6 ? kScaleX : kScaleB);
+      }
+#pragma unroll
+      for (int o = 0; o < O; ++o) {
+        const float w = (float)raw[7 + o] * (ok ? 1.f : 0.f);
+        n.w2[p][o][h] = w;
+        acc[o] += fabsf(w) * (3.f * r + 5.f + (float)out_roundings<L, U>());
+      }
+    }
+    if ((p + 1) % PG_LOAD_BATCH == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+  WT rawc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) rawc[o] = g[off2 + (long)o * (H + b) + (b ? H : 0)];
+  float e = 0.f;
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    n.c[o] = (float)rawc[o] * (b ? 1.f : 0.f);
+    e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + (float)out_roundings<L, U>() * fabsf(n.c[o])));
+  }
+  n.e = e;
+}
+
+// Hidden layer and the lane-partial output sums of one packed network; k are
+// the six doubled-centroid features (x_i = k_i / 320 is folded into W1).
+template <int U, int O>
+__device__ __forceinline__ void partial_pk(const NetP<U, O> &n, const int k[6], float acc[O]) {
+  constexpr int P = NetP<U, O>::P;
+  float2v kx[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const float f = (float)k[i];
+    kx[i] = float2v{f, f};
+  }
+  float2v a2[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) a2[o] = float2v{0.f, 0.f};
+  // two unit pairs per step: their dependent pk_fma chains interleave, so the
+  // wait state a packed op owes its dependent successor is filled with work
+#pragma unroll
+  for (int p = 0; p < P; p += 2) {
+    constexpr int kStep = 2;
+    const bool two = p + 1 < P;
+    float2v a = n.w1[p][6], b = two ? n.w1[p + 1][6] : float2v{0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      a = __builtin_elementwise_fma(n.w1[p][i], kx[i], a);
+      if (two) b = __builtin_elementwise_fma(n.w1[p + 1][i], kx[i], b);
+    }
+    const float2v qa = float2v{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
+    const float2v qb = float2v{__builtin_amdgcn_exp2f(b.x), __builtin_amdgcn_exp2f(b.y)} + 1.0f;
+    const float2v sa = float2v{__builtin_amdgcn_rcpf(qa.x), __builtin_amdgcn_rcpf(qa.y)};
+    const float2v sb = float2v{__builtin_amdgcn_rcpf(qb.x), __builtin_amdgcn_rcpf(qb.y)};
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      a2[o] = __builtin_elementwise_fma(n.w2[p][o], sa, a2[o]);
+      if (two) a2[o] = __builtin_elementwise_fma(n.w2[p + 1][o], sb, a2[o]);
+    }
+    (void)kStep;
+  }
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = a2[o].x + a2[o].y;
+}
+
+// Certified argmax of S(z) = 1/(1 + pow(e, -z)) in f64 (numpy_nn.py:22-23,131)
+// given |z_true - z[o]| <= e.  S is exactly 1.0 iff z >= 53 ln 2 =
+// 36.73680056967710 (then every saturated output ties and the first wins);
+// below that S rounds onto plateaus no wider than 2^-52 (e^z + 1) in z (x4
+// margin below).  Returns -1 when the bound cannot prove the f64 decision;
+// the caller then recomputes the forward pass in f64.
+template <int O>
+__device__ __forceinline__ int certify(const float z[O], float e) {
+  // Branch-free: (a) the first output that may be saturated decides if it
+  // surely is (it ties at 1.0 with every later saturated one and beats every
+  // unsaturated one); (b) with none possibly saturated, the f32 winner must
+  // lead the runner-up by 2e plus the plateau width at its value.
+  constexpr float kTlo = 36.7367f, kThi = 36.7369f;
+  constexpr float kLowZ = -708.0f;
+  int sat_res = -2;  // -2: no output may be saturated
+#pragma unroll
+  for (int o = O - 1; o >= 0; --o) {
+    const bool maybe = !(z[o] + e < kTlo);  // NaN counts as "maybe"
+    const bool sure = z[o] - e > kThi;
+    sat_res = maybe ? (sure ? o : -1) : sat_res;
+  }
+  float top1 = z[0], top2 = -3.0e38f;
+  int w = 0;
+#pragma unroll
+  for (int o = 1; o < O; ++o) {
+    const bool gt = z[o] > top1;
+    top2 = gt ? top1 : fmaxf(top2, z[o]);
+    w = gt ? o : w;
+    top1 = gt ? z[o] : top1;
+  }
+  const float tw = 8.8817842e-16f * (__expf(fminf(top1 + e, 40.f)) + 1.0f);
+  // the gap rule needs the winner's S(z) normal: below z = -1022 ln 2 it is
+  // subnormal (coarse steps), and 0.0 for every z < -709.78 (pow overflows),
+  // where all such outputs tie and the first wins -- the f64 path decides there
+  const int uns_res = (top1 - top2 > 2.f * e + tw && top1 - e > kLowZ) ? w : -1;
+  float sum = 0.f;
+#pragma unroll
+  for (int o = 0; o < O; ++o) sum += z[o];
+  if (sum != sum) return -1;  // a NaN output (non-finite weights): numpy's NaN rule in f64
+  return sat_res != -2 ? sat_res : uns_res;
+}
+
+// The f64 re-decision of one forward pass by the L lanes of a group, in
+// numpy's order: every dot product as np.dot runs it (blas_dot: OpenBLAS
+// dgemv_t's summation), every sigmoid correctly rounded (pg_sigmoid_f64).
+// Hidden units are strided over the lanes; the output rows are staged in LDS
+// by all lanes (coalesced) and lane o < O sums output o out of LDS -- no
+// serial global loads.
+// LDS: lds[0, H) hidden activations, lds[H + o*(H+1) + j] output weights,
+// then O output activations (f64_out_offset); f64_lds_doubles(H, O) doubles.
+__host__ __device__ constexpr int f64_lds_doubles(int H, int O) { return H + O * (H + 1) + O + 1; }
+__host__ __device__ constexpr int f64_out_offset(int H, int O) { return H + O * (H + 1); }
+
+template <int L, int U, int O, typename WT>
+__device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H, int b, const double *x, double *lds,
+                                              int lig) {
+  const int cols = 6 + b;
+#pragma unroll 1
+  for (int j = lig; j < H; j += L) {
+    const WT *row = g + (long)j * cols;
+    double w[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w[i] = (i < 6 || b) ? (double)row[i] : 0.0;
+    lds[j] = pg_sigmoid_f64(blas_dot6(w, x, b));
+  }
+  double *w2 = lds + H;
+  const WT *v = g + (long)H * cols;
+#pragma unroll 1
+  for (int t = lig; t < O * (H + b); t += L) {
+    const int o = t / (H + b), j = t - o * (H + b);
+    w2[o * (H + 1) + j] = (double)v[(long)o * (H + b) + j];
+  }
+  wave_lds_sync();
+  double *out = lds + f64_out_offset(H, O);
+  if (lig < O) {
+    const double *wr = w2 + lig * (H + 1);
+    const double z = blas_dot([&](int j) { return wr[j]; }, [&](int j) { return j < H ? lds[j] : 1.0; }, H + b,
+                              blas_kind(lig, O));
+    out[lig] = pg_sigmoid_f64(z);
+  }
+  wave_lds_sync();
+  int best = 0;  // np.argmax: the first NaN if any, else the first maximum
+  for (int o = 1; o < O && !__builtin_isnan(out[best]); ++o)
+    if (__builtin_isnan(out[o]) || out[o] > out[best]) best = o;
+  wave_lds_sync();
+  return best;
+}
+
+// The same from the doubled-centroid features k (utils.inference's values).
+template <int L, int U, int O, typename WT>
+__device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H, int b, const int *k, double *lds,
+                                              int lig) {
+  double x[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
+  return forward_f64_group<L, U, O, WT>(g, H, b, (const double *)x, lds, lig);
+}
+
+__device__ __forceinline__ float feat32(int k) { return (float)k * 0.003125f; }  // k / 320, <= 2u rel. error
+
+// One frame's decisions: the right paddle's network always, the left paddle's
+// when it is a network too (self-play / hall-of-fame games).  The two f32
+// passes are independent, so their hidden layers and reductions interleave.
+// Any undecided argmax is re-decided by ONE f64 code site (keeps the rare
+// path's registers and code out of the hot loop's way).
+template <int L, int U, int O, typename WT>
+__device__ __forceinline__ int2 decide(Net<U, O> &nr, const WT *gr, const int kr[6], Net<U, O> &nl,
+                                       const WT *gl, const int kl[6], bool left_nn, int left_scripted, int H,
+                                       int b, double *lds, int lig, uint32_t &slow) {
+  float xr[6], ar[O], zr[O], zl[O];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) xr[i] = feat32(kr[i]);
+  partial_f32<U, O>(nr, xr, ar);
+  int il = 0;
+  if (left_nn) {
+    float xl[6], al[O];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) xl[i] = feat32(kl[i]);
+    partial_f32<U, O>(nl, xl, al);
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      zr[o] = group_sum<L>(ar[o]) + nr.c[o];
+      zl[o] = group_sum<L>(al[o]) + nl.c[o];
+    }
+    il = certify<O>(zl, nl.e);
+  } else {
+#pragma unroll
+    for (int o = 0; o < O; ++o) zr[o] = group_sum<L>(ar[o]) + nr.c[o];
+  }
+  int ir = certify<O>(zr, nr.e);
+#ifdef PG_ABLATE_CERT  // timing-only build: plain f32 argmax, no certification
+  ir = zr[1] > zr[0] ? 1 : 0;
+  if (left_nn) il = zl[1] > zl[0] ? 1 : 0;
+#endif
+  if (ir < 0 || il < 0) {  // rare and group-uniform
+    if (il < 0) {
+      il = forward_f64_group<L, U, O, WT>(gl, H, b, kl, lds, lig);
+      slow += 1;
+    }
+    if (ir < 0) {
+      ir = forward_f64_group<L, U, O, WT>(gr, H, b, kr, lds, lig);
+      slow += 1;
+    }
+    // Re-read the weights instead of keeping them live across the f64 pass:
+    // the rare path then does not add its registers to the hot loop's budget.
+    load_net<L, U, O, WT>(nr, gr, H, b, lig);
+    if (left_nn) load_net<L, U, O, WT>(nl, gl, H, b, lig);
+  }
+  return make_int2(index_to_code(ir), left_nn ? index_to_code(il) : left_scripted);
+}
+
+template <int L>
+__device__ __forceinline__ int group_broadcast(int v, int leader_lane) {
+  if constexpr (L == 64) return __builtin_amdgcn_readfirstlane(v);
+  return __shfl(v, leader_lane, 64);
+}
+
+// ================================================ split-lane helpers ==
+template <int L>
+__device__ __forceinline__ int other_half(int v) {
+  if constexpr (L == 8) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror: i <-> 7-i
+  } else if constexpr (L == 16) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror: i <-> 15-i
+  } else if constexpr (L == 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
+  }
+}
+
+// ============================================ split lanes + f64 service wave ==
+// k_split's layout, with the rare f64 re-decision moved to a dedicated wave:
+// a block (svc_threads) runs its game waves and ONE service wave.  A half-group
+// whose certificate fails posts {genome, features} to an LDS mailbox and
+// sleeps until the service wave (64 lanes, numpy_nn order, f64) answers.  The
+// f64 code then lives in its own control-flow region, so it no longer sets
+// the game waves' register budget (which decides their occupancy).
+// Block size by register budget: a game lane holds 10U + 4 weight floats, so
+// U <= 4 fits 128 VGPRs (4 waves/SIMD: 16-wave blocks), U = 8 fits 168
+// (3 waves/SIMD: 12-wave blocks), U = 16 fits 256 (2 waves/SIMD: 8-wave blocks).
+// One block per CU either way; PG_SVC_NT forces one size (experiments).
+template <int U>
+__host__ __device__ constexpr int svc_threads() {
+#ifdef PG_SVC_NT
+  return PG_SVC_NT;
+#else
+  return U <= 4 ? 1024 : (U <= 8 ? 768 : 512);
+#endif
+}
+
+// A game whose rally settles into a periodic orbit meets the same near-tie
+// states every period; without a memo each costs a round trip to the service
+// wave (~3 us), and such games ran 3-4x slower per frame and set the launch's
+// tail (tools/timeline.py).  The memo holds the network's last kMemo f64
+// decisions keyed by the packed features -- the decision is a pure function
+// of (network, features), so a hit is exact.  Cleared at every game start.
+constexpr int kMemo = 8;
+
+struct SlowSlot {
+  const void *g;    // genome row of the network to re-decide
+  int k[6];         // its doubled-centroid features
+  float z[4];       // the f32 output pre-activations and their bound e
+  float e;
+  int idx;          // answer: argmax index
+  volatile int flag;  // 0 free, 1 posted, 2 answered
+  volatile int n_memo;  // decisions memoised for the current game's network
+  volatile uint64_t memo_key[kMemo];
+  volatile int memo_idx[kMemo];
+  uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
+  int rally_at, rally_span;
+};
+
+// The plateau certificate in f32, tried by the game wave itself where
+// certify() failed (no round trip to the service wave).  Same rule as
+// plateau_decide below, but m(z) = rint(2^52 pow(e, -z)) is only bracketed:
+// v = exp2(52 - z log2 e) in f32 is within 2e-5 v of 2^52 e^-z (exponent
+// rounding <= (|t| + 2 |z| log2 e) u, v_exp_f32 ~1 ulp, x4 margin), so
+// ceil(v(z + e) - d - 1/2) <= m_true <= floor(v(z - e) + d + 1/2).  Useful
+// where v is small (z >~ 28); near 22 the bracket is wide and the service
+// decides.
+template <int O>
+__device__ __forceinline__ int plateau_f32(const float z[O], float e) {
+  constexpr int kBelow = 0x7ffffff0;  // S below the plateau regime (z < 22)
+  constexpr int kNone = 0x7fffffff;   // cannot bracket
+  int mlo[O], mhi[O];
+  bool bad = false;
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    const float zl = z[o] - e, zh = z[o] + e;
+    bad = bad || !(zl == zl);  // NaN
+    // upper bracket of m from the low end z - e (valid when z - e >= 22.2)
+    if (zl >= 22.2f) {
+      const float v = __builtin_amdgcn_exp2f(fmaf(-zl, 1.44269504f, 52.f));
+      mhi[o] = (int)floorf(v * (1.f + 2e-5f) + 0.5f);
+    } else {
+      mhi[o] = kNone;
+    }
+    // lower bracket of m from the high end z + e
+    if (zh >= 22.2f) {
+      const float v = __builtin_amdgcn_exp2f(fmaf(-zh, 1.44269504f, 52.f));
+      mlo[o] = (int)ceilf(v * (1.f - 2e-5f) - 0.5f);
+    } else {
+      mlo[o] = zh < 22.0f ? kBelow : -1;  // -1: straddles the regime edge, never "surely below"
+    }
+  }
+  if (bad) return -1;
+  int res = -1;
+#pragma unroll
+  for (int w = O - 1; w >= 0; --w) {
+    bool ok = mhi[w] != kNone;
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+      if (o != w) ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
+    res = ok ? w : res;
+  }
+  return res;
+}
+
+// Plateau certificate, tried first by the service wave (no memory traffic).
+// For z >= 22.2, numpy's S(z) = 1/(1 + pow(e, -z)) is exactly
+// 1 - m(z) 2^-52 with m(z) = rint(2^52 pow(e, -z)) (1 + p rounds to
+// 1 + m 2^-52; its reciprocal rounds to 1 - m 2^-52 while m < 2^20), so two
+// outputs tie iff their m are equal and the larger S is the smaller m.  m is
+// monotone in z, so with |z_true - z| <= e the f32 outputs bound each m
+// between m(z + e) and m(z - e).  This decides the near-saturation rallies
+// whose plateaus are too wide for certify()'s gap test.  Lanes 0..2O-1 each
+// evaluate one endpoint; returns -1 when undecided (the full f64 path runs).
+template <int O>
+__device__ int plateau_decide(const float *z, float e, int lane) {
+  constexpr int kBig = 0x7fffffff;  // "below the plateau regime": worse than any m
+  int m = kBig;
+  bool amb = false;
+  if (lane < 2 * O) {
+    float zo = z[0];  // z[lane >> 1] without a dynamic (scratch) index
+#pragma unroll
+    for (int o = 1; o < O; ++o) zo = (lane >> 1) == o ? z[o] : zo;
+    const double zz = (double)zo + ((lane & 1) ? (double)e : -(double)e);
+    if (zz != zz) {
+      amb = true;  // NaN: numpy's NaN rule, in the f64 path
+    } else if (zz >= 22.2) {
+      double t = pg_exp_f64(-zz);
+      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
+      const double v = t * 4503599627370496.0;    // 2^52 p
+      const double fr = v - floor(v);
+      amb = fabs(fr - 0.5) < 1e-6;  // too close to a rounding boundary to call
+      m = (int)rint(v);
+    }
+  }
+  if (__ballot(amb)) return -1;
+  int mlo[O], mhi[O];  // m(z + e) <= m_true <= m(z - e)
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    mhi[o] = __builtin_amdgcn_readlane(m, 2 * o);
+    mlo[o] = __builtin_amdgcn_readlane(m, 2 * o + 1);
+  }
+#pragma unroll
+  for (int w = 0; w < O; ++w) {
+    bool ok = mhi[w] != kBig;
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+      if (o != w) ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
+    if (ok) return w;
+  }
+  return -1;
+}
+
+// Certified f64 decision, tried by the service wave before the numpy-order
+// f64 forward.  The wave evaluates the network in f64 in parallel (one hidden
+// unit per lane, tree sums) and bounds its distance to numpy's own f64 result
+// z_np (numpy_nn.py:120-131: sequential dot products, bias last):
+//   |z - z_np| <= e_o = 2 eps (sum_j |W2_oj| (4 A_j + 84) + 2 |c_o|),
+// eps = 2^-53, A_j = sum_i |W1_ji x_i| + |b_j| -- both dot products within
+// gamma_7 A_j of the exact one, slope <= 1/4, both sigmoids within 6 ulp,
+// both output sums within gamma_66 + gamma_8 of exact, x2 margin.  That is
+// ~1e-11, ten orders below the f32 bound, so the decision is almost always
+// provable; with O outputs on lanes:
+//  * for z >= 22.2, S_np(z) = 1 - m(z) 2^-52 exactly, m(z) = rint(2^52
+//    pow(e, -z)) (1 + p rounds to 1 + m 2^-52, whose reciprocal rounds to
+//    1 - m 2^-52 while m < 2^20); m is monotone, so [z - e, z + e] bounds m
+//    between m(z + e) and m(z - e); ties are equal m, larger S is smaller m;
+//  * below that, S is strictly increasing on gaps above the plateau width
+//    4 2^-52 (e^z + 1), so a gap test decides.
+// Returns -1 when undecided (NaN, a rounding boundary within 1e-6 of m's
+// half-integer, or a tie the intervals cannot settle).
+// Sum of a double over the 64 lanes (DPP within rows, permlane swaps across).
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#define PG_DPP64(CTRL)                                                                          \
+  {                                                                                           \
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);                                  \
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)bits, CTRL, 0xF, 0xF, false); \
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(bits >> 32), CTRL, 0xF, 0xF, false); \
+    v += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));                        \
+  }
+  PG_DPP64(0xB1) PG_DPP64(0x4E) PG_DPP64(0x141) PG_DPP64(0x140)
+#undef PG_DPP64
+  {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)bits, (uint32_t)bits, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(bits >> 32), (uint32_t)(bits >> 32), false, false);
+    v = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0])) +
+        __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+  }
+  {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)bits, (uint32_t)bits, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(bits >> 32), (uint32_t)(bits >> 32), false, false);
+    v = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0])) +
+        __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+  }
+  return v;
+}
+
+template <int O, typename WT>
+__device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int *k, int lane) {
+  constexpr double kEps = 1.1102230246251565e-16;  // 2^-53
+  double x[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
+  const int cols = 6 + b;
+  const WT *v = g + (long)H * cols;
+  double zp[O], ep[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) { zp[o] = 0.0; ep[o] = 0.0; }
+#pragma unroll 1
+  for (int j = lane; j < H; j += 64) {
+    const WT *row = g + (long)j * cols;
+    double a = b ? (double)row[6] : 0.0;
+    double A = fabs(a);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double w = (double)row[i];
+      a = fma(w, x[i], a);
+      A = fma(fabs(w), x[i], A);
+    }
+    // the compact sigmoid (pow(e_d, -a) as exp(-a)(1 + a delta), ~1-2 ulp; the
+    // bound above allows 6): no table load on the service's critical path
+    double tq = pg_exp_f64(-a);
+    if (tq < INFINITY) tq = fma(tq, a * 5.318237706605891e-17, tq);
+    const double sj = 1.0 / (1.0 + tq);
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      const double w2 = (double)v[(long)o * (H + b) + j];
+      zp[o] = fma(w2, sj, zp[o]);
+      ep[o] = fma(fabs(w2), 4.0 * A + 84.0, ep[o]);
+    }
+  }
+  double z[O], e[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    const double t = wave_sum_f64(zp[o]);  // any order: e covers it
+    const double u = wave_sum_f64(ep[o]);
+    const double c = b ? (double)v[(long)o * (H + b) + H] : 0.0;
+    z[o] = t + c;
+    e[o] = 2.0 * kEps * (u + 2.0 * fabs(c)) * 1.001 + 1e-300;
+  }
+  // m-intervals: lanes 0..2O-1 each evaluate one endpoint (z -/+ e)
+  constexpr int kBig = 0x7fffffff;  // below the plateau regime
+  int m = kBig;
+  bool amb = false;
+  if (lane < 2 * O) {
+    double zo = z[0], eo = e[0];
+#pragma unroll
+    for (int o = 1; o < O; ++o)
+      if ((lane >> 1) == o) { zo = z[o]; eo = e[o]; }
+    const double zz = (lane & 1) ? zo + eo : zo - eo;
+    if (zz != zz) {
+      amb = true;  // NaN: numpy's NaN rule, in the full path
+    } else if (zz >= 22.2) {
+      double t = pg_exp_f64(-zz);
+      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
+      const double vv = t * 4503599627370496.0;   // 2^52 p
+      amb = fabs(vv - floor(vv) - 0.5) < 1e-6;
+      m = (int)rint(vv);
+    } else if (zz >= 22.0) {
+      amb = true;  // too close to the regime edge to compare across it
+    }
+  }
+  if (__ballot(amb)) return -1;
+  int mlo[O], mhi[O];  // m(z + e) <= m_np <= m(z - e)
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    mhi[o] = __builtin_amdgcn_readlane(m, 2 * o);
+    mlo[o] = __builtin_amdgcn_readlane(m, 2 * o + 1);
+  }
+#pragma unroll
+  for (int w = 0; w < O; ++w) {
+    bool ok = true;
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      if (o == w) continue;
+      if (mhi[w] != kBig) {  // w surely in the plateau regime
+        ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
+      } else {  // S_w below the regime: a strict gap above the plateau width
+        const double top = z[w] + e[w];
+        const double tw = 8.881784197001252e-16 * (pg_exp_f64(fmin(top, 40.0)) + 1.0);
+        // and S_w normal (z > -1022 ln 2; S = 0.0 for all z < -709.78, see certify)
+        ok = ok && (z[w] - e[w] > z[o] + e[o] + tw) && (z[w] - e[w] > -708.0);
+      }
+    }
+    if (ok) return w;
+  }
+  return -1;
+}
+
+// the six doubled-centroid features, each in [0, 512), as one 54-bit key
+__device__ __forceinline__ uint64_t memo_key(const int k[6]) {
+  uint64_t key = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) key = (key << 9) | (uint64_t)(k[i] & 511);
+  return key;
+}
+
+}  // namespace pg

@@ -48,10 +48,13 @@ struct EvalParams {
   int n_nodes, bias, max_width;
 };
 
-// Genome blocks / games this launch plays (pg_eval_args.n_active).
+// Genome blocks / games this launch plays (pg_eval_args.n_active).  Made
+// wave-uniform explicitly: as a per-lane load result the loop bound of the
+// game loops became a vector compare, which cost k_service 14 % (11.0 vs
+// 12.7 ms per launch, tools/runs/r2_b6.sh).
 __device__ inline int active_genomes(const EvalParams &p) {
   if (!p.n_active) return p.n_genomes;
-  const int a = *p.n_active;
+  const int a = __builtin_amdgcn_readfirstlane(*p.n_active);
   return a < 0 ? 0 : (a < p.n_genomes ? a : p.n_genomes);
 }
 __device__ inline int active_total(const EvalParams &p) {
@@ -110,5 +113,11 @@ __device__ inline void log_hard(const EvalParams &p, int row, int is_opp, int id
 // n_games <= 8) on the weight-streaming kernel k_wide (pg_wide.hip).
 bool wide_shape_ok(const pg_net &n, int n_games);
 int32_t launch_wide(const EvalParams &p, int dtype, hipStream_t s);
+
+// [6, H<=256, 2..4] networks on the two-stage kernel k_staged (pg_staged.hip):
+// its extra workspace (prepared lane records of every row) and the launch.
+bool staged_shape_ok(const pg_net &n);
+size_t staged_workspace_bytes(const pg_eval_args *a);
+int32_t launch_staged(const EvalParams &p, const pg_eval_args *a, void *prep, hipStream_t s);
 
 }  // namespace pg

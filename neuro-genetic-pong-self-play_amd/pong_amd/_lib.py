@@ -24,7 +24,7 @@ PG_F32, PG_F64 = 0, 1
 PG_OPP_HARDCODED, PG_OPP_ROM_CPU, PG_OPP_SCORE, PG_OPP_NN = 0, 1, 2, 3
 PG_PREC_CERTIFIED, PG_PREC_F64 = 0, 1
 PG_SCHED_REFERENCE, PG_SCHED_SELFPLAY = 0, 1
-PG_KERNEL_AUTO, PG_KERNEL_GENERAL, PG_KERNEL_RESIDENT, PG_KERNEL_SPLIT, PG_KERNEL_WIDE = 0, 1, 2, 3, 4
+PG_KERNEL_AUTO, PG_KERNEL_GENERAL, PG_KERNEL_RESIDENT, PG_KERNEL_SPLIT, PG_KERNEL_WIDE, PG_KERNEL_STAGED = 0, 1, 2, 3, 4, 5
 PG_STATE_FIELDS = 16
 STATE_FIELD_NAMES = ("ball_x", "ball_y", "ball_vx", "ball_vy", "ball_visible", "serve_timer",
                      "serve_dir", "hits", "point", "lpy", "rpy", "score1", "score2",

@@ -16,7 +16,7 @@ from . import _lib as L
 
 PRECISIONS = {"certified": L.PG_PREC_CERTIFIED, "f64": L.PG_PREC_F64}
 KERNELS = {"auto": L.PG_KERNEL_AUTO, "general": L.PG_KERNEL_GENERAL, "resident": L.PG_KERNEL_RESIDENT,
-           "split": L.PG_KERNEL_SPLIT, "wide": L.PG_KERNEL_WIDE}
+           "split": L.PG_KERNEL_SPLIT, "wide": L.PG_KERNEL_WIDE, "staged": L.PG_KERNEL_STAGED}
 DTYPES = {torch.float32: L.PG_F32, torch.float64: L.PG_F64}
 
 

@@ -1,0 +1,142 @@
+"""k_staged (PG_KERNEL_STAGED, csrc/pg_staged.hip) against the oracle and the
+reference's own episode traces, and against k_service at full size.
+
+The staged kernel plays the same games as k_service with each frame split
+into an environment stage (one lane per game) and a network stage; every
+result must be bit-identical to the oracle's (scores, frames, total_frames,
+rewards, fitness, status) and to k_service's.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import _assert_same, _dev_genomes, _gene_count, _run_both, _schedule
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape", [[6, 2, 2], [6, 8, 3], [6, 37, 3], [6, 64, 3], [6, 64, 2], [6, 64, 4],
+                                   [6, 100, 3], [6, 200, 4]])
+@pytest.mark.parametrize("dist", ["init", "n3"])
+def test_staged_matches_oracle(gpu, oracle, shape, dist):
+    from pong_amd.device import Evaluator
+    rng = np.random.default_rng(sum(shape) * 3 + (0 if dist == "init" else 5))
+    G = _gene_count(shape)
+    n, H = 131, 17  # ragged: not a multiple of the 56 slots of a block
+    draw = (lambda s: rng.random(s)) if dist == "init" else (lambda s: rng.standard_normal(s) * 3.0)
+    genomes, opponents = draw((n, G)), draw((H, G))
+    kinds, opp, mult = _schedule(rng, n, 6, H)
+    ev = Evaluator(shape, device=gpu, kernel="staged")
+    res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
+    _assert_same(res, ref)
+    c = res.counters.cpu().numpy()
+    assert int(c[0]) + int(c[8]) == int(ref["frames"].sum())
+    assert int(c[3]) == n * 6
+
+
+def test_staged_f32_genomes(gpu, oracle):
+    from pong_amd.device import Evaluator
+    shape = [6, 64, 3]
+    rng = np.random.default_rng(12)
+    G = _gene_count(shape)
+    genomes = rng.standard_normal((70, G)).astype(np.float32).astype(np.float64) * 3
+    opponents = rng.standard_normal((9, G)).astype(np.float32).astype(np.float64) * 3
+    kinds, opp, mult = _schedule(rng, 70, 6, 9)
+    ev = Evaluator(shape, device=gpu, dtype=torch.float32, kernel="staged")
+    res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
+    _assert_same(res, ref)
+
+
+def test_staged_near_saturation(gpu, oracle):
+    """The bench distribution: the f32 certificate fails often; the environment
+    wave's plateau rule, certified f64, memo and numpy-order forward decide."""
+    from pong_amd.device import Evaluator
+    shape = [6, 64, 3]
+    rng = np.random.default_rng(5)
+    G = _gene_count(shape)
+    n, H = 1536, 384
+    genomes = rng.standard_normal((n, G)) * 3.0
+    opponents = genomes[:H]
+    kinds = np.full((n, 6), 3, np.int32)
+    opp = ((np.arange(n)[:, None] * 6 + np.arange(6)[None, :]) % H).astype(np.int32)
+    mult = np.ones((n, 6))
+    ev = Evaluator(shape, device=gpu, kernel="staged")
+    res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
+    _assert_same(res, ref)
+    c = res.counters.cpu().numpy()
+    assert c[4] > 0 and c[5] > 0 and c[6] > 0, c
+    assert c[8] > 0, c
+    assert c[2] + c[5] + c[6] <= c[4], c
+
+
+def test_staged_episode_traces_match_reference(gpu, golden):
+    """Per-frame actions of the REAL perform_episode (tests/golden/episodes.json)."""
+    from pong_amd.device import Evaluator
+    for ep in golden("episodes.json"):
+        shape = ep["shape"]
+        n_games = ep["game_index"] + 1
+        ev = Evaluator(shape, device=gpu, n_games=n_games, kernel="staged")
+        G = _gene_count(shape)
+        kinds = np.zeros((1, n_games), np.int32)
+        kinds[0, ep["game_index"]] = ep["kind"]
+        opp = np.zeros((1, n_games), np.int32)
+        mult = np.ones((1, n_games))
+        mult[0, ep["game_index"]] = ep["mult"]
+        opponents = np.array([ep["opp"]]) if ep["opp"] is not None else np.zeros((1, G))
+        cap = ep["frames"] + 1
+        res, trace = ev.evaluate(_dev_genomes(np.array([ep["right"]]), gpu), torch.tensor(kinds, device=gpu),
+                                 torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
+                                 opponents=_dev_genomes(opponents, gpu), trace_games=n_games, trace_cap=cap)
+        gi = ep["game_index"]
+        assert int(res.frames[0, gi]) == ep["frames"]
+        assert float(res.rewards[0, gi]) == ep["reward"]
+        tr = trace[gi, : ep["frames"]].cpu().numpy()
+        np.testing.assert_array_equal(tr[:-1] & 3, np.array(ep["right_actions"][1:]))
+        np.testing.assert_array_equal((tr[:-1] >> 2) & 3, np.array(ep["left_actions"][1:]))
+
+
+def test_staged_without_opponents_and_with_rows(gpu, oracle):
+    """No opponents tensor (scripted games only), then genome_rows + n_active."""
+    from pong_amd.device import Evaluator
+    shape = [6, 64, 3]
+    rng = np.random.default_rng(21)
+    G = _gene_count(shape)
+    genomes = rng.standard_normal((40, G)) * 2
+    kinds = np.tile(np.array([0, 1, 2, 0, 1, 2], np.int32), (40, 1))
+    ev = Evaluator(shape, device=gpu, kernel="staged")
+    dev_g = _dev_genomes(genomes, gpu)
+    res, _ = ev.evaluate(dev_g, torch.tensor(kinds, device=gpu), torch.zeros((40, 6), dtype=torch.int32, device=gpu),
+                         torch.ones((40, 6), dtype=torch.float64, device=gpu))
+    ref = oracle.eval_population(genomes, shape, kinds, np.zeros((40, 6)), np.ones((40, 6)))
+    np.testing.assert_array_equal(res.fitness.cpu().numpy(), ref["fitness"])
+    np.testing.assert_array_equal(res.frames.cpu().numpy(), ref["frames"])
+    # rows: evaluate rows [5, 3, 39, 0, 7] of the genomes, only the first 4 entries active
+    rows = torch.tensor([5, 3, 39, 0, 7], dtype=torch.int32, device=gpu)
+    n_active = torch.tensor([4], dtype=torch.int32, device=gpu)
+    k5 = torch.tensor(kinds[:5], device=gpu)
+    res2, _ = ev.evaluate(dev_g, k5, torch.zeros((5, 6), dtype=torch.int32, device=gpu),
+                          torch.ones((5, 6), dtype=torch.float64, device=gpu), rows=rows, n_active=n_active)
+    sel = [5, 3, 39, 0]
+    np.testing.assert_array_equal(res2.fitness[:4].cpu().numpy(), ref["fitness"][sel])
+    assert int(res2.counters[3]) == 4 * 6
+
+
+def test_staged_equals_split_full_size(gpu):
+    """pop 65 536, [6,64,3] self-play (the bench workload): k_staged and
+    k_service return identical results and simulate the same frames."""
+    from pong_amd.device import Evaluator
+    shape = [6, 64, 3]
+    n, H = 65536, 16384
+    G = _gene_count(shape)
+    gen = torch.Generator(device=gpu).manual_seed(99)
+    genomes = torch.randn((n, G), generator=gen, dtype=torch.float64, device=gpu) * 3.0
+    opponents = genomes[:H].contiguous()
+    ev = Evaluator(shape, device=gpu)
+    kind, opp, mult = ev.selfplay_schedule(n, H)
+    r1, _ = ev.evaluate(genomes, kind, opp, mult, opponents=opponents, kernel="split")
+    r2, _ = ev.evaluate(genomes, kind, opp, mult, opponents=opponents, kernel="staged")
+    for name in ("fitness", "rewards", "scores", "frames", "total_frames", "status"):
+        assert torch.equal(getattr(r1, name), getattr(r2, name)), name
+    c1, c2 = r1.counters.cpu().numpy(), r2.counters.cpu().numpy()
+    assert c1[0] == c2[0] and c1[1] == c2[1] and c1[3] == c2[3] and c1[8] == c2[8], (c1, c2)
+    assert c1[4] == c2[4] and c1[6] == c2[6], (c1, c2)  # the same certificate failures, same in-wave rule
