@@ -1,3 +1,8 @@
+# This module restates part of DEAP (Distributed Evolutionary Algorithms in Python,
+# https://github.com/DEAP/deap, Copyright (C) the DEAP developers), which is
+# distributed under the GNU Lesser General Public License v3 or later.  The call
+# order and messages follow DEAP on purpose (a seeded run must draw the same
+# random numbers as DEAP would); this file is therefore LGPL-3.0-or-later.
 """DEAP's creator / base / tools / algorithms, restated (deap is not installed
 and there is no package index).  Used by ga.py only when ``import deap``
 fails.  It follows DEAP's published algorithms (deap 1.3/1.4: eaSimple,

@@ -1,3 +1,8 @@
+# This module restates part of DEAP (Distributed Evolutionary Algorithms in Python,
+# https://github.com/DEAP/deap, Copyright (C) the DEAP developers), which is
+# distributed under the GNU Lesser General Public License v3 or later.  The call
+# order and messages follow DEAP on purpose (a seeded run must draw the same
+# random numbers as DEAP would); this file is therefore LGPL-3.0-or-later.
 """deap.base restated: Toolbox and Fitness (used at ga.py:77,80)."""
 from collections.abc import Sequence
 from copy import deepcopy

@@ -1,3 +1,8 @@
+# This module restates part of DEAP (Distributed Evolutionary Algorithms in Python,
+# https://github.com/DEAP/deap, Copyright (C) the DEAP developers), which is
+# distributed under the GNU Lesser General Public License v3 or later.  The call
+# order and messages follow DEAP on purpose (a seeded run must draw the same
+# random numbers as DEAP would); this file is therefore LGPL-3.0-or-later.
 """deap.creator restated: ``create(name, base, **attrs)`` makes a class in
 this module's namespace (so instances pickle), e.g. ga.py:80-81."""
 import warnings

@@ -1,8 +1,15 @@
-"""Worker for tests/test_gpu_dist.py: a few DeviceGA generations with the
+"""Worker for tests/test_gpu_dist.py: DeviceGA generations with the
 population sharded over WORLD_SIZE ranks (gloo; every rank on cuda:0), rank 0
-saves the final state.  usage: python _dist_ga_worker.py OUT_DIR"""
+saves the final state.
+
+usage: python _dist_ga_worker.py OUT_DIR            (small: [6,8,3], P 101, 3 generations)
+       python _dist_ga_worker.py OUT_DIR config4    (BASELINE config 4: [6,64,3], P 524 288,
+                                                     self-play vs P/4 hall of fame, 2 generations)
+"""
+import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -10,28 +17,74 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "neuro-genetic-pong-self-play_amd"))
 
 
-def main(out_dir):
+def main(out_dir, mode="small"):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         dist.init_process_group("gloo")
+    from pong_amd import device as D
     from pong_amd.evolve import DeviceGA
-    ga = DeviceGA([6, 8, 3], 101, hof_size=20, tournsize=9, device=torch.device("cuda", 0),
-                  schedule="reference", seed=77)
-    ga.initialize("normal", 2.0)
-    ga.run(3)
-    if not dist.is_initialized() or dist.get_rank() == 0:
-        os.makedirs(out_dir, exist_ok=True)
-        np.save(os.path.join(out_dir, "population.npy"), ga.population.cpu().numpy())
-        np.save(os.path.join(out_dir, "fitness.npy"), ga.fitness.cpu().numpy())
-        np.save(os.path.join(out_dir, "hof.npy"), ga.hall_of_fame.cpu().numpy())
-        np.save(os.path.join(out_dir, "hof_fitness.npy"), ga.hof_member_fitness)
-        np.save(os.path.join(out_dir, "rows.npy"), np.array([ga.lo, ga.hi]))
+    dev = torch.device("cuda", 0)
+    if mode == "config4":
+        P = 524288
+        ga = DeviceGA([6, 64, 3], P, device=dev, schedule="selfplay", seed=4)
+        ga.initialize("normal", 3.0)
+        sample = {}
+
+        def keep(g, rows, opponents, res):  # the last evaluation's inputs for 48 of this rank's rows
+            n = res.fitness.shape[0]
+            rng = np.random.default_rng(g)
+            pick = np.sort(rng.choice(n, size=min(48, n), replace=False))
+            pt = torch.as_tensor(pick, device=dev)
+            r = ga.last_rows[pt].long() if ga.last_rows is not None else pt  # rows: full offspring / the shard
+            kind, opp, mult = D.schedule(ga.schedule, ga.hi - ga.lo, ga.n_games, ga.lo, ga.hof_fitness, ga.hof_n,
+                                         ga.seed, g, dev, rows=ga.last_rows)
+            o = opp[pt].cpu().numpy()
+            used = np.unique(o)  # only the hall-of-fame rows these games play
+            opp_rows = (opponents[torch.as_tensor(used, device=dev)].double().cpu().numpy()
+                        if opponents is not None else None)
+            sample.update(genomes=rows[r].double().cpu().numpy(), kind=kind[pt].cpu().numpy(),
+                          opp=np.searchsorted(used, o).astype(np.int32), mult=mult[pt].cpu().numpy(),
+                          opponents=opp_rows,
+                          fitness=res.fitness[pt].cpu().numpy(), frames=res.frames[pt].cpu().numpy(),
+                          played=(torch.arange(n, device=dev)[pt] < (ga.last_count[0] if ga.last_count is not None
+                                                                      else n)).cpu().numpy())
+        ga.on_evaluate = keep
+        ga.step()              # generation 0: the initial evaluation
+        ga.profile = {}        # generation 1 phases (synchronised per phase)
+        t0 = time.perf_counter()
+        ga.step()
+        torch.cuda.synchronize()
+        step_ms = (time.perf_counter() - t0) * 1e3
+        phases = dict(ga.profile)
+        ga.profile = None
+        if not dist.is_initialized() or dist.get_rank() == 0:
+            os.makedirs(out_dir, exist_ok=True)
+            h = D.row_hash(ga.population, ga.G).cpu().numpy()
+            np.save(os.path.join(out_dir, "pop_hash.npy"), h)
+            np.save(os.path.join(out_dir, "fitness.npy"), ga.fitness.cpu().numpy())
+            np.save(os.path.join(out_dir, "hof_hash.npy"), D.row_hash(ga.hall_of_fame, ga.G).cpu().numpy())
+            np.save(os.path.join(out_dir, "hof_fitness.npy"), ga.hof_member_fitness)
+            np.savez(os.path.join(out_dir, "sample.npz"), **{k: v for k, v in sample.items() if v is not None})
+            with open(os.path.join(out_dir, "profile.json"), "w") as fh:
+                json.dump({"world": world, "rank_rows": ga.hi - ga.lo, "generation1_ms": step_ms,
+                           "generation1_phases_ms": phases, "logbook": ga.logbook}, fh)
+    else:
+        ga = DeviceGA([6, 8, 3], 101, hof_size=20, tournsize=9, device=dev, schedule="reference", seed=77)
+        ga.initialize("normal", 2.0)
+        ga.run(3)
+        if not dist.is_initialized() or dist.get_rank() == 0:
+            os.makedirs(out_dir, exist_ok=True)
+            np.save(os.path.join(out_dir, "population.npy"), ga.population.cpu().numpy())
+            np.save(os.path.join(out_dir, "fitness.npy"), ga.fitness.cpu().numpy())
+            np.save(os.path.join(out_dir, "hof.npy"), ga.hall_of_fame.cpu().numpy())
+            np.save(os.path.join(out_dir, "hof_fitness.npy"), ga.hof_member_fitness)
+            np.save(os.path.join(out_dir, "rows.npy"), np.array([ga.lo, ga.hi]))
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "small")

@@ -22,14 +22,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(world, out):
+def _run(world, out, *extra, timeout=240):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     if world == 1:
-        cmd = [sys.executable, WORKER, out]
+        cmd = [sys.executable, WORKER, out, *extra]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-               "--master-addr=127.0.0.1", f"--master-port={_port()}", WORKER, out]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+               "--master-addr=127.0.0.1", f"--master-port={_port()}", WORKER, out, *extra]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
 
@@ -43,3 +43,37 @@ def test_sharded_device_ga_equals_single_process(gpu, tmp_path):
     for world in (2, 3):
         for k in outs[1]:
             np.testing.assert_array_equal(outs[world][k], outs[1][k], err_msg=f"{k} at world {world}")
+
+
+def test_config4_sharded_524k_equals_single_process(gpu, oracle, tmp_path):
+    """BASELINE config 4 readiness: population 524 288, [6,64,3] self-play vs a
+    131 072-row hall of fame, two generations (the initial evaluation and one
+    eaSimple step), sharded over 8 gloo ranks on cuda:0 (the N = 8 code path:
+    rank shards, one all-gather of fitness per generation) -- equal to the
+    single-process run row for row, and 48 of rank 0's evaluated genomes
+    re-played by the oracle."""
+    import json
+    outs = {}
+    for world in (1, 8):
+        out = str(tmp_path / f"c4w{world}")
+        _run(world, out, "config4", timeout=600)
+        outs[world] = {k: np.load(os.path.join(out, f"{k}.npy"))
+                       for k in ("pop_hash", "fitness", "hof_hash", "hof_fitness")}
+        with open(os.path.join(out, "profile.json")) as fh:
+            outs[world]["profile"] = json.load(fh)
+        if world == 8:
+            smp = dict(np.load(os.path.join(out, "sample.npz")))
+    for k in ("pop_hash", "fitness", "hof_hash", "hof_fitness"):
+        np.testing.assert_array_equal(outs[8][k], outs[1][k], err_msg=k)
+    assert outs[8]["profile"]["logbook"] == outs[1]["profile"]["logbook"]
+    played = smp["played"].astype(bool)
+    assert played.sum() > 0
+    ref = oracle.eval_population(smp["genomes"][played], [6, 64, 3], smp["kind"][played], smp["opp"][played],
+                                 smp["mult"][played], opponents=smp["opponents"], n_threads=8)
+    np.testing.assert_array_equal(smp["fitness"][played], ref["fitness"])
+    np.testing.assert_array_equal(smp["frames"][played], ref["frames"])
+    rec = {w: outs[w]["profile"] for w in (1, 8)}
+    repo = os.path.dirname(HERE)
+    if os.path.isdir(os.path.join(repo, "gpurun_out")):
+        with open(os.path.join(repo, "gpurun_out", "config4_profile.json"), "w") as fh:
+            json.dump(rec, fh, indent=1)
