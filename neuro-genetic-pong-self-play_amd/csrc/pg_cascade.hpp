@@ -47,6 +47,15 @@ struct Net {
   float e;         // certified bound on |z_o(f32) - z_o(exact)|, max over outputs
 };
 
+// A network whose f32 weights could overflow an f32 sum (or are NaN / inf)
+// gets the bound e = inf: certify() then never decides and the f64 path
+// (numpy's semantics, NaN rule included) does.  With each lane's sum of
+// |weights| <= kWeightCap (a sum, so NaN and inf propagate) no f32
+// pre-activation or output can overflow or become NaN, so the per-frame
+// certificate needs no NaN test.
+constexpr float kWeightCap = 1e30f;
+__device__ __forceinline__ bool weights_ok(float big) { return big <= kWeightCap; }  // false for NaN
+
 // Loads the [6, H, O] genome's weights for this lane (numpy_nn.py:52-69
 // layout: layer l is a row-major (out, in + bias) block, bias column last) and
 // computes the error bound of the f32 output pre-activations:
@@ -59,6 +68,7 @@ __device__ __forceinline__ void load_net(Net<U, O> &n, const WT *__restrict__ g,
   const int cols = 6 + b;
   const long off2 = (long)H * cols;
   float acc[O];
+  float big = 0.f;  // sum of this lane's |weights|: NaN / inf / huge -> see kWeightCap
 #pragma unroll
   for (int o = 0; o < O; ++o) acc[o] = 0.f;
 #pragma unroll
@@ -86,6 +96,9 @@ __device__ __forceinline__ void load_net(Net<U, O> &n, const WT *__restrict__ g,
       n.w2[u][o] = (float)raw[7 + o] * (ok ? 1.f : 0.f);
       acc[o] += fabsf(n.w2[u][o]) * (3.f * r + 18.f);
     }
+    big += r;
+#pragma unroll
+    for (int o = 0; o < O; ++o) big += fabsf(n.w2[u][o]);
     // bound the loads in flight (f64: 2 VGPRs each): this cold spot would
     // otherwise set the register budget of the whole kernel
     if ((u + 1) % PG_LOAD_BATCH == 0) __builtin_amdgcn_sched_barrier(0);
@@ -97,9 +110,12 @@ __device__ __forceinline__ void load_net(Net<U, O> &n, const WT *__restrict__ g,
 #pragma unroll
   for (int o = 0; o < O; ++o) {
     n.c[o] = (float)rawc[o] * (b ? 1.f : 0.f);
-    e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + 13.f * fabsf(n.c[o])));
+    big += fabsf(n.c[o]);
   }
-  n.e = e;
+#pragma unroll
+  for (int o = 0; o < O; ++o) e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + 13.f * fabsf(n.c[o])));
+  // any lane of the group over the cap (or NaN): the whole network is f64-decided
+  n.e = group_sum<L>(weights_ok(big) ? 0.f : 1.f) > 0.f ? __builtin_inff() : e;
 }
 
 __device__ __forceinline__ float sigmoid_f32(float a) {
@@ -151,14 +167,24 @@ __host__ __device__ constexpr int out_roundings() {
   return U + (HL >= 32 ? 5 : HL >= 16 ? 4 : HL >= 8 ? 3 : HL >= 4 ? 2 : HL >= 2 ? 1 : 0) + 3;
 }
 
+// flip (the left paddle's network in k_service): the x-flip and me/enemy
+// swap of get_actions (main.py:146-147) folded into the weights, so both
+// halves of a group read the same feature vector k = [bx, by, lbx, lby, right,
+// left]: the left network sees x = [1 - k0, k1, 1 - k2, k3, k5, k4] (x320),
+// i.e. W'0 = -W0, W'2 = -W2, W'4 = W5, W'5 = W4 and bias' = bias + W0 + W2,
+// folded in f64 and rounded to f32 once -- an f32 network of the same exact
+// pre-activations, so the bound below (computed from the folded weights)
+// covers it; the f64 fold error (<= 2^-51 R_j) fits the 3u R_j term's slack.
 template <int L, int U, int O, typename WT>
-__device__ __forceinline__ void load_net_pk(NetP<U, O> &n, const WT *__restrict__ g, int H, int b, int lig) {
+__device__ __forceinline__ void load_net_pk(NetP<U, O> &n, const WT *__restrict__ g, int H, int b, int lig,
+                                            int flip = 0) {
   constexpr int P = NetP<U, O>::P;
   constexpr float kScaleX = -1.4426950408889634f / 320.f;
   constexpr float kScaleB = -1.4426950408889634f;
   const int cols = 6 + b;
   const long off2 = (long)H * cols;
   float acc[O];
+  float big = 0.f;
 #pragma unroll
   for (int o = 0; o < O; ++o) acc[o] = 0.f;
 #pragma unroll
@@ -174,18 +200,32 @@ __device__ __forceinline__ void load_net_pk(NetP<U, O> &n, const WT *__restrict_
       for (int i = 0; i < 7; ++i) raw[i] = g[(long)jj * cols + ((i < 6 || b) ? i : 0)];
 #pragma unroll
       for (int o = 0; o < O; ++o) raw[7 + o] = g[off2 + (long)o * (H + b) + jj];
+      float wf[7];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) wf[i] = (float)raw[i] * ((ok && (i < 6 || b)) ? 1.f : 0.f);
+      if (flip) {  // only the bias is folded in f64 (one rounding); the rest are exact f32 moves
+        const double bias = (((ok && b) ? (double)raw[6] : 0.0) + (ok ? (double)raw[0] : 0.0)) +
+                            (ok ? (double)raw[2] : 0.0);
+        const float w4 = wf[4];
+        wf[0] = -wf[0];
+        wf[2] = -wf[2];
+        wf[4] = wf[5];
+        wf[5] = w4;
+        wf[6] = (float)bias;
+      }
       float r = 0.f;
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
-        const float w = (float)raw[i] * ((ok && (i < 6 || b)) ? 1.f : 0.f);
-        r += fabsf(w);
-        n.w1[p][i][h] = w * (i < 6 ? kScaleX : kScaleB);
+        r += fabsf(wf[i]);
+        n.w1[p][i][h] = wf[i] * (i < 6 ? kScaleX : kScaleB);
       }
+      big += r;
 #pragma unroll
       for (int o = 0; o < O; ++o) {
         const float w = (float)raw[7 + o] * (ok ? 1.f : 0.f);
         n.w2[p][o][h] = w;
         acc[o] += fabsf(w) * (3.f * r + 5.f + (float)out_roundings<L, U>());
+        big += fabsf(w);
       }
     }
     if ((p + 1) % PG_LOAD_BATCH == 0) __builtin_amdgcn_sched_barrier(0);
@@ -197,9 +237,13 @@ __device__ __forceinline__ void load_net_pk(NetP<U, O> &n, const WT *__restrict_
 #pragma unroll
   for (int o = 0; o < O; ++o) {
     n.c[o] = (float)rawc[o] * (b ? 1.f : 0.f);
-    e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + (float)out_roundings<L, U>() * fabsf(n.c[o])));
+    big += fabsf(n.c[o]);
   }
-  n.e = e;
+#pragma unroll
+  for (int o = 0; o < O; ++o)
+    e = fmaxf(e, 2.f * kU * (group_sum<L>(acc[o]) + (float)out_roundings<L, U>() * fabsf(n.c[o])));
+  // any lane of the group over the cap (or NaN): the whole network is f64-decided
+  n.e = group_sum<L>(weights_ok(big) ? 0.f : 1.f) > 0.f ? __builtin_inff() : e;
 }
 
 // Hidden layer and the lane-partial output sums of one packed network; k are
@@ -273,15 +317,13 @@ __device__ __forceinline__ int certify(const float z[O], float e) {
     w = gt ? o : w;
     top1 = gt ? z[o] : top1;
   }
-  const float tw = 8.8817842e-16f * (__expf(fminf(top1 + e, 40.f)) + 1.0f);
+  // (top1 + e < kTlo whenever this rule is used: no saturated output)
+  const float tw = 8.8817842e-16f * (__expf(top1 + e) + 1.0f);
   // the gap rule needs the winner's S(z) normal: below z = -1022 ln 2 it is
   // subnormal (coarse steps), and 0.0 for every z < -709.78 (pow overflows),
   // where all such outputs tie and the first wins -- the f64 path decides there
   const int uns_res = (top1 - top2 > 2.f * e + tw && top1 - e > kLowZ) ? w : -1;
-  float sum = 0.f;
-#pragma unroll
-  for (int o = 0; o < O; ++o) sum += z[o];
-  if (sum != sum) return -1;  // a NaN output (non-finite weights): numpy's NaN rule in f64
+  // no NaN test: outputs are finite whenever e is (weights_ok at load time)
   return sat_res != -2 ? sat_res : uns_res;
 }
 

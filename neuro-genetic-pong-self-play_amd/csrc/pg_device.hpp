@@ -72,8 +72,10 @@ struct Pong {
   }
 
   // env.step(action) (main.py:77): right [up,down] = action[4:6], left = action[6:8].
-  // Branch-free except the serve (once per point): every game of a lane group
-  // runs the same instruction stream, so divergent branches would cost both sides.
+  // The common case -- the ball in flight, away from both paddle faces -- is
+  // straight-line code; reaching a face (bounce or miss, ~1 frame in 40 of a
+  // game) and the hidden-ball countdown are branches.  The lanes of a group
+  // play one game, so a branch only costs the waves where some game takes it.
   __device__ void step(int right_code, int left_code) {
     rpy = move(rpy, dy_of(right_code), kPaddleSpeed);
     // left paddle: the action, or the built-in CPU of the 1-player env (main.py:40)
@@ -81,42 +83,46 @@ struct Pong {
     const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
     lpy = move(lpy, one_player ? cpu_dy : dy_of(left_code), one_player ? kCpuSpeed : kPaddleSpeed);
 
-    // ball in play: move, walls, paddle faces
     constexpr int ymax = kFieldH - kBallH;
     constexpr int lface = kLeftPaddleX + kPaddleW, rface = kRightPaddleX;
-    int nx = bx + vx, ny = by + vy;
-    const bool wall_top = ny < 0, wall_bot = ny > ymax;
-    ny = wall_top ? -ny : (wall_bot ? 2 * ymax - ny : ny);
-    const int wvy = (wall_top || wall_bot) ? -vy : vy;
-    const bool to_left = (vx < 0) && (nx <= lface - 1);
-    const bool to_right = (vx > 0) && (nx + kBallW - 1 >= rface);
-    const int py = to_left ? lpy : rpy;
-    const bool overlap = (ny <= py + kPaddleH - 1) && (ny + kBallH - 1 >= py);
-    const bool hit = vis && (to_left || to_right) && overlap;
-    const bool miss = vis && (to_left || to_right) && !overlap;
-    const int nhits = hits + (hit ? 1 : 0);
-    const int mag = min(kBallVx0 + (nhits >> 2), kBallVxMax);
-    // (2 (ny - py) - 12) / 6 truncated toward zero; |d| <= 18 is even, so |d| / 6 == (|d| * 43) >> 8
-    const int d = 2 * (ny - py) - 12;
-    const int q = (abs(d) * 43) >> 8;
-    const int hvy = d < 0 ? -q : q;
-    if (vis && !miss) {  // a miss leaves the ball where it was (hidden until the serve)
-      bx = hit ? (to_left ? lface : rface - kBallW) : nx;
-      by = ny;
-      vx = hit ? (to_left ? mag : -mag) : vx;
-      vy = hit ? hvy : wvy;
+    if (vis) {
+      // ball in play: move, walls
+      const int nx = bx + vx;
+      int ny = by + vy;
+      const bool wall_top = ny < 0, wall_bot = ny > ymax;
+      ny = wall_top ? -ny : (wall_bot ? 2 * ymax - ny : ny);
+      const int wvy = (wall_top || wall_bot) ? -vy : vy;
+      const bool to_left = (vx < 0) && (nx <= lface - 1);
+      const bool to_right = (vx > 0) && (nx + kBallW - 1 >= rface);
+      if (__builtin_expect(to_left || to_right, 0)) {  // crossing a paddle face: bounce or miss
+        const int py = to_left ? lpy : rpy;
+        if ((ny <= py + kPaddleH - 1) && (ny + kBallH - 1 >= py)) {  // rows overlap: bounce
+          hits += 1;
+          const int mag = min(kBallVx0 + (hits >> 2), kBallVxMax);
+          // (2 (ny - py) - 12) / 6 truncated toward zero; |d| <= 18 is even, so |d| / 6 == (|d| * 43) >> 8
+          const int d = 2 * (ny - py) - 12;
+          const int q = (abs(d) * 43) >> 8;
+          bx = to_left ? lface : rface - kBallW;
+          by = ny;
+          vx = to_left ? mag : -mag;
+          vy = d < 0 ? -q : q;
+        } else {  // a miss scores for the other side; the ball stays, hidden until the next serve
+          s2 += to_left ? 1 : 0;
+          s1 += to_right ? 1 : 0;
+          dir = to_left ? -1 : 1;
+          timer = kServeDelay;
+          vis = 0;
+        }
+      } else {
+        bx = nx;
+        by = ny;
+        vy = wvy;
+      }
+    } else {
+      // ball hidden: the serve timer runs down (the frame of a miss only starts it)
+      timer = timer > 0 ? timer - 1 : 0;
+      if (timer == 0 && !done()) serve();
     }
-    hits = nhits;
-    // a miss scores for the other side and hides the ball until the next serve
-    s2 += (miss && to_left) ? 1 : 0;
-    s1 += (miss && to_right) ? 1 : 0;
-    dir = miss ? (to_left ? -1 : 1) : dir;
-    // ball hidden: the serve timer runs down (the frame of a miss only starts it)
-    const int t = vis ? timer : (timer > 0 ? timer - 1 : 0);
-    timer = miss ? kServeDelay : t;
-    const bool do_serve = !vis && t == 0 && !done();
-    vis = (vis && !miss) ? 1 : 0;
-    if (do_serve) serve();
   }
 
   __device__ void serve() {

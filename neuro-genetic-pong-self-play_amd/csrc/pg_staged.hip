@@ -315,10 +315,13 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
       if (lane == 0) __hip_atomic_fetch_add(&done_cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #ifdef PG_STAGED_PROFILE
-    if (wave == 0 && lane == 0 && p.trace) {
+    if (lane == 0 && p.trace) {
       uint64_t *d = (uint64_t *)(p.trace + (long)blockIdx.x * p.trace_cap);
-      d[5] = prof[5];
-      d[6] = prof[6];
+      if (wave == 0) {
+        d[5] = prof[5];
+        d[6] = prof[6];
+      }
+      d[16 + wave] = prof[5];  // every network wave's compute cycles
     }
 #endif
     if (p.counters) {

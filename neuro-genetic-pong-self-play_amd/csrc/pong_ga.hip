@@ -382,7 +382,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       kind = p.kind[w];
       const WT *gr = genomes + (long)genome_row(p, i) * p.gstride;
       gm = (side && kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
-      load_net_pk<HL, U, O, WT>(net, gm, H, b, hl);
+      load_net_pk<HL, U, O, WT>(net, gm, H, b, hl, side);  // the left network with the x-flip folded in
       st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
       act_r = act_l = timeout = total = frames = 0;
       fresh = false;
@@ -402,9 +402,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     int left = 0, right = 0;
     if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
       const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
-      // right side: [bx, by, lbx, lby, me=right, enemy=left]; left side x-flipped (main.py:146-147)
-      const int k[6] = {side ? 320 - bx2 : bx2, by2, side ? 320 - lbx2 : lbx2, lby2, side ? lc2 : rc2,
-                        side ? rc2 : lc2};
+      // [bx, by, lbx, lby, me = right, enemy = left] for both halves: the left
+      // network's x-flip and me/enemy swap (main.py:146-147) are in its weights
+      const int k[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
       float acc[O], z[O];
       partial_pk<U, O>(net, k, acc);
 #pragma unroll
@@ -434,9 +434,12 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           idx = hit;
         } else {
           if (hl == 0) {
+            // the network's own features (x-flipped for the left paddle): the f64 path uses the genes
+            const int kn[6] = {side ? 320 - bx2 : bx2, by2, side ? 320 - lbx2 : lbx2, lby2, side ? lc2 : rc2,
+                               side ? rc2 : lc2};
             slots[sx].g = gm;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) slots[sx].k[i] = k[i];
+            for (int i = 0; i < 6; ++i) slots[sx].k[i] = kn[i];
 #pragma unroll
             for (int o = 0; o < O; ++o) slots[sx].z[o] = z[o];
             slots[sx].e = net.e;
@@ -464,16 +467,21 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       const int mine = index_to_code(idx);
       const int other = other_half<L>(mine);
       right = side ? other : mine;
-      int scripted = hardcoded(by2, lc2);
-      if (kind == kOppScore && st.s1 > st.s2) scripted = 0;
-      left = left_nn ? (side ? mine : other) : scripted;
+      if (left_nn) {
+        left = side ? mine : other;
+      } else {  // HardcodedAi / ScoreHardcodedAi (dumb_ais.py), group-uniform: skipped in self-play
+        left = hardcoded(by2, lc2);
+        if (kind == kOppScore && st.s1 > st.s2) left = 0;
+      }
       c_fwd += left_nn ? 2 : 1;
     }
     act_l = clamp_action(lc2, left);
     act_r = clamp_action(rc2, right);
 #ifndef PG_TIMELINE
-    if (p.trace && w < p.trace_games && frames <= p.trace_cap && lig == 0)
-      p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+    if (p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
+      if (w < p.trace_games && frames <= p.trace_cap && lig == 0)
+        p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+    }
 #endif
     if (frames > 1) {
       if (st.s1 == s1b && st.s2 == s2b) {

@@ -8,7 +8,8 @@ The kernel then writes per-block cycle counts into the trace buffer:
 [2] service cycles, [3] env cycles wait + phase C + phase A, [4] env barrier
 cycles, [5] net wave 0 compute cycles, [6] net wave 0 barrier cycles,
 [7] block cycles, [8] playing slot-frames, [9] visible slot-frames,
-[10] requests served, [11] env cycles before the wait (overlapped start pipeline).
+[10] requests served, [11] env cycles before the wait (overlapped start pipeline),
+[16 + w] network wave w's compute cycles.
 usage: PONG_GA_LIB=variants/lib_prof.so python tools/staged_probe.py
 """
 import json
@@ -36,10 +37,10 @@ def main():
     for rep in range(2):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        res, tr = ev.evaluate(genomes, kind, opp, mult, opponents=hof, trace_games=nb, trace_cap=128, validate=False)
+        res, tr = ev.evaluate(genomes, kind, opp, mult, opponents=hof, trace_games=nb, trace_cap=256, validate=False)
         b.record()
         torch.cuda.synchronize()
-    d = tr.cpu().numpy().view(np.uint64).reshape(nb, 16).astype(np.float64)
+    d = tr.cpu().numpy().view(np.uint64).reshape(nb, 32).astype(np.float64)
     fr = d[:, 0]
     out = {"kernel_ms": a.elapsed_time(b), "blocks": nb, "frames_per_block_mean": float(fr.mean()),
            "frames_per_block_max": float(fr.max()), "block_cycles_mean": float(d[:, 7].mean()),
@@ -53,6 +54,7 @@ def main():
     out["playing_slots_per_frame"] = float(d[:, 8].sum() / fr.sum())
     out["visible_slots_per_frame"] = float(d[:, 9].sum() / fr.sum())
     out["requests_per_frame"] = float(d[:, 10].sum() / fr.sum())
+    out["net_wave_compute_per_frame"] = [float(d[:, 16 + w].sum() / fr.sum()) for w in range(7)]
     out["env_steps"] = int(res.counters[0])
     print(json.dumps(out, indent=1))
 
