@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
   __shared__ StagedReq req[2 * NS];
   __shared__ StagedMemo memo[2 * NS];
   __shared__ f4v stg[kStagedLoads][STG4];
-  __shared__ int done_cnt;
+  __shared__ int sync_word;  // network waves done (<< 16) + requests posted, this frame
   __shared__ int exit_flag;
   extern __shared__ double lds_svc[];  // f64_lds_doubles(H, O): the numpy-order forward
 
@@ -213,10 +213,13 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
   }
   if (threadIdx.x < NS) rec[threadIdx.x] = 0;
   if (threadIdx.x == 0) {
-    lds_st(&done_cnt, 0);
+    lds_st(&sync_word, 0);
     lds_st(&exit_flag, 0);
   }
 #ifdef PG_STAGED_PROFILE
+  __shared__ unsigned long long t_done_max;
+  if (threadIdx.x == 0) t_done_max = 0;
+  uint64_t t_release = 0;
   uint64_t prof[16];
   for (int i = 0; i < 16; ++i) prof[i] = 0;
   PG_PT(t_begin);
@@ -304,6 +307,7 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
             dec[sl] = kPend;
             __threadfence_block();
             lds_st(&req[sl].flag, 1);
+            __hip_atomic_fetch_add(&sync_word, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
             dec[sl] = index_to_code(idx);
           }
@@ -312,7 +316,10 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
       __threadfence_block();
       PG_PT(tb2);
       PG_PADD(5, tb2 - tb1);
-      if (lane == 0) __hip_atomic_fetch_add(&done_cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef PG_STAGED_PROFILE
+      if (lane == 0) atomicMax(&t_done_max, (unsigned long long)tb2);
+#endif
+      if (lane == 0) __hip_atomic_fetch_add(&sync_word, 1 << 16, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #ifdef PG_STAGED_PROFILE
     if (lane == 0 && p.trace) {
@@ -375,6 +382,30 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
     // network waves compute; the registers they fill are first read below.
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     PG_PT(te0);
+
+    // ---- (T) last step's decision-independent bookkeeping (main.py:94-107,
+    // 128-135): the no-score counter and termination need the scores after
+    // the step, not this frame's decisions, so they run before the wait; a
+    // game that ended frees its slot for this frame's claim
+    bool fin_now = false;
+    const int w_traced = w;
+    if (state == kSlotPlaying) {
+      if (frames > 1) {  // calculate_timeout_and_frames main.py:128-135
+        if (st.s1 == s1b && st.s2 == s2b) {
+          timeout += 1;
+        } else {
+          total += timeout;
+          timeout = 0;
+        }
+      }
+      if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
+        finish_game_m(p, w, st, frames, total, mult);
+        c_steps += frames;
+        c_games += 1;
+        state = kSlotEmpty;
+        fin_now = true;
+      }
+    }
 
     // ---- (a) records loaded last frame -> this frame's staging buffers; those games start now
     uint32_t reload = 0;
@@ -457,9 +488,16 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
     if (!first) {
       // ---- wait for the network stage, serving certificate failures meanwhile
       PG_PT(tw0);
+      // one LDS word per poll: requests posted (low half) and network waves done
+      // (high half); a request's flag is set before its count, so a scan after
+      // seeing the count finds it
+      int n_served = 0;
       for (;;) {
-        const bool done = lds_ld(&done_cnt) == kStagedNetWaves;  // read before the scan: posts precede the count
-        bool served = false;
+        const int sw = lds_ld(&sync_word);
+        if ((sw & 0xFFFF) == n_served) {
+          if ((sw >> 16) == kStagedNetWaves) break;
+          continue;  // spin: the network stage is short and this wave has nothing else to do
+        }
         for (int base = 0; base < 2 * NS; base += 64) {
           const int i = base + lane;
           const bool posted = i < 2 * NS && lds_ld(&req[i].flag) == 1;
@@ -468,7 +506,7 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
             const int rs = base + __builtin_ctzll(mask);
             mask &= mask - 1;
             __threadfence_block();
-            served = true;
+            n_served += 1;
             PG_PT(ts0);
             int k[6];
 #pragma unroll
@@ -516,16 +554,22 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
             PG_PADD(10, 1);
           }
         }
-        if (done && !served) break;
-        if (!served) __builtin_amdgcn_s_sleep(1);
       }
       __threadfence_block();
       PG_PT(te1);
       PG_PADD(1, te1 - tw0);
       PG_PADD(11, tw0 - te0);
+#ifdef PG_STAGED_PROFILE
+      {
+        const uint64_t tdm = t_done_max;
+        PG_PADD(12, te1 - tdm);         // done seen after the last network wave finished
+        PG_PADD(13, tdm - t_release);   // network stage span from the barrier release
+      }
+#endif
 
-      // ---- apply the decisions: get_actions, bounds, bookkeeping, termination
-      if (state == kSlotPlaying) {
+      // ---- apply the decisions: get_actions, bounds, the rally jump (the
+      // decision-independent bookkeeping of this frame ran before the wait)
+      if (state == kSlotPlaying || fin_now) {
         int left = 0, right = 0;
         if (vis) {
           const bool lnn = kind == kOppNN;
@@ -537,20 +581,12 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
         }
         act_l = clamp_action(lc2, left);
         act_r = clamp_action(rc2, right);
-        if (tracing && w < p.trace_games && frames <= p.trace_cap)
-          p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
-        if (frames > 1) {  // calculate_timeout_and_frames main.py:128-135
-          if (st.s1 == s1b && st.s2 == s2b) {
-            timeout += 1;
-          } else {
-            total += timeout;
-            timeout = 0;
-          }
-        }
+        if (tracing && w_traced < p.trace_games && frames <= p.trace_cap)
+          p.trace[(long)w_traced * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
 #ifndef PG_NO_RALLY_SKIP
         // a periodic rally ends at the timeout with nothing else changed: jump there
-        if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
-            !tracing) {
+        if (state == kSlotPlaying && timeout >= kRallyStart && timeout <= kTimeoutThresh &&
+            (timeout & (kRallyStride - 1)) == 0 && !tracing) {
           const uint64_t key = rally_key(st, act_r, act_l);
           if (timeout == kRallyStart) {
             rkey = key;
@@ -561,6 +597,10 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
             frames += rest;
             skipped += rest;
             timeout = kTimeoutThresh + 1;
+            finish_game_m(p, w, st, frames, total, mult);  // main.py:105: ends at the timeout
+            c_steps += frames;
+            c_games += 1;
+            state = kSlotEmpty;
           } else if (timeout - rat == rspan) {
             rkey = key;
             rat = timeout;
@@ -568,12 +608,6 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
           }
         }
 #endif
-        if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
-          finish_game_m(p, w, st, frames, total, mult);
-          c_steps += frames;
-          c_games += 1;
-          state = kSlotEmpty;
-        }
       }
     }
     first = false;
@@ -606,7 +640,7 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
     }
     if (lane < NS) rec[lane] = r;
     const bool alive = __ballot(state != kSlotDrained) != 0;
-    lds_st(&done_cnt, 0);
+    lds_st(&sync_word, 0);
     if (!alive) lds_st(&exit_flag, 1);
     parity ^= 1;
 #ifdef PG_STAGED_PROFILE
@@ -615,11 +649,15 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
     PG_PADD(8, __popcll(__ballot(state == kSlotPlaying)));
     PG_PADD(9, __popcll(__ballot(state == kSlotPlaying && vis)));
 #endif
+#ifdef PG_STAGED_PROFILE
+    if (lane == 0) t_done_max = 0;
+#endif
     __syncthreads();
 #ifdef PG_STAGED_PROFILE
     PG_PT(te3);
     PG_PADD(3, te2 - te0);
     PG_PADD(4, te3 - te2);
+    t_release = te3;
 #endif
     if (!alive) break;
   }
@@ -629,6 +667,7 @@ __global__ __launch_bounds__(kStagedThreads) void k_staged(EvalParams p, const f
     uint64_t *d = (uint64_t *)(p.trace + (long)blockIdx.x * p.trace_cap);
     d[0] = prof[0]; d[1] = prof[1]; d[2] = prof[2]; d[3] = prof[3]; d[4] = prof[4];
     d[7] = t_end - t_begin; d[8] = prof[8]; d[9] = prof[9]; d[10] = prof[10]; d[11] = prof[11];
+    d[12] = prof[12]; d[13] = prof[13];
   }
 #endif
   if (p.counters) {

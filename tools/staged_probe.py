@@ -46,7 +46,7 @@ def main():
            "frames_per_block_max": float(fr.max()), "block_cycles_mean": float(d[:, 7].mean()),
            "cycles_per_frame": float((d[:, 7] / np.maximum(fr, 1)).mean())}
     names = {1: "env_wait", 2: "service", 3: "env_frame_to_barrier", 4: "env_barrier", 5: "net0_compute",
-             6: "net0_barrier", 11: "env_pre_wait"}
+             6: "net0_barrier", 11: "env_pre_wait", 12: "done_detect_lag", 13: "net_stage_span"}
     for i, nm in names.items():
         out[nm + "_per_frame"] = float(d[:, i].sum() / fr.sum())
     out["env_C_A_per_frame"] = (out["env_frame_to_barrier_per_frame"] - out["env_wait_per_frame"]
