@@ -27,6 +27,7 @@ Shims (all documented in DESIGN.md "Oracle"):
     ``fitness.valid/values`` (deap is absent).
 
 Usage:  python tests/golden/make_golden.py   (takes a few minutes)
+        python tests/golden/make_golden.py episodes_s3 wide_s3   (the round-2 additions)
         python tests/golden/make_golden.py hard_cases gpurun_out/.../hard_cases.npz
         (nn_hard_cases.npz from a tools/harvest_hard.py run on the GPU)
 """
@@ -433,6 +434,105 @@ def gen_episodes():
         json.dump(eps, fh)
 
 
+def gen_episodes_s3():
+    """More perform_episode traces at the bench's gene scale ([6,64,3], N(0, 3)):
+    every game slot of evaluate() (0 HardcodedAi, 1 the ROM CPU, 2
+    ScoreHardcodedAi, 3-5 network opponents with negative and fractional
+    right_score_multiplier), long rallies, and games that end at the
+    2 000-frame timeout -- the periodic rallies the kernels jump over when
+    not tracing.  Candidates are screened with the CPU oracle (the build's
+    physics) and then played by the REAL perform_episode."""
+    rng = np.random.default_rng(303)
+    shape = [6, 64, 3]
+    G = gene_count(shape)
+    kinds = [O.OPP_HARDCODED, O.OPP_ROM_CPU, O.OPP_SCORE, O.OPP_NN, O.OPP_NN, O.OPP_NN]
+    picked = []  # (slot, right, opp, mult, tag)
+    # quotas: 2 games per slot; 6 timeouts and 6 long rallies (500-2000
+    # frames), at least 3 of each against a network opponent; no two picks
+    # with the same slot, frames and score (N(0, 3) networks often saturate to
+    # one action and replay the same game)
+    quota = {"slot": [2] * 6, "timeout": 6, "long": 6, "timeout_nn": 3, "long_nn": 3}
+    seen = set()
+    tries = 0
+    while tries < 20000 and (max(quota["slot"]) > 0 or quota["timeout"] > 0 or quota["long"] > 0):
+        tries += 1
+        slot = tries % 6
+        right = rng.standard_normal(G) * 3.0
+        opp = rng.standard_normal(G) * 3.0
+        mult = float(np.round(rng.uniform(-1.5, 1.0), 3)) if kinds[slot] == O.OPP_NN else 1.0
+        r = O.play_game(right, shape, kinds[slot], opp if kinds[slot] == O.OPP_NN else None, mult,
+                        seed=O.game_seed(0, slot))
+        sig = (slot, r["frames"], r["score1"], r["score2"])
+        if sig in seen:
+            continue
+        nn = kinds[slot] == O.OPP_NN
+        tag = None
+        for t, ok in (("timeout", r["frames"] > 2000), ("long", 500 <= r["frames"] <= 2000)):
+            # keep room for the network-opponent share of each quota
+            if ok and quota[t] > 0 and (nn or quota[t] > quota[t + "_nn"]):
+                tag = t
+                quota[t] -= 1
+                if nn:
+                    quota[t + "_nn"] = max(0, quota[t + "_nn"] - 1)
+                break
+        if tag is None and quota["slot"][slot] > 0:
+            tag = "slot"
+            quota["slot"][slot] -= 1
+        if tag is None:
+            continue
+        seen.add(sig)
+        picked.append((slot, right, opp, mult, tag))
+    eps = []
+    for slot, right, opp, mult, tag in picked:
+        ns = make_namespace(shape)
+        kind = kinds[slot]
+        env = FakeEnv(slot, one_player=(kind == O.OPP_ROM_CPU))
+        right_model = ref_utils.create_model_from_genes(list(right))
+        if kind == O.OPP_NN:
+            left_model = ref_utils.create_model_from_genes(list(opp))
+        elif kind == O.OPP_SCORE:
+            left_model = ref_dumb.ScoreHardcodedAi()
+        else:
+            left_model = ref_dumb.HardcodedAi()
+        env.reset()
+        reward = ns["perform_episode"](env, left_model, right_model, False, mult)
+        rec = np.array(env.received, dtype=np.int64)
+        st = env.last_info
+        eps.append(dict(shape=shape, dist="n3", kind=kind, game_index=slot, mult=mult, tag=tag,
+                        right=right.tolist(), opp=opp.tolist() if kind == O.OPP_NN else None,
+                        right_actions=(rec[:, 4] + 2 * rec[:, 5]).tolist(),
+                        left_actions=(rec[:, 6] + 2 * rec[:, 7]).tolist(),
+                        frames=len(env.received), score1=st["score1"], score2=st["score2"],
+                        reward=float(reward)))
+        print(f"episode s3 slot={slot} {tag}: frames={len(env.received)} "
+              f"score={st['score1']}-{st['score2']} reward={reward}", flush=True)
+    with open(os.path.join(HERE, "episodes_s3.json"), "w") as fh:
+        json.dump(eps, fh)
+
+
+def gen_wide_s3():
+    """NeuralNetwork.run of the wide net at the wide bench's gene scale (N(0, 3)),
+    16 inputs each on the game's k/320 grid, seeds 9 and 10."""
+    shape = [6, 512, 512, 3]
+    G = gene_count(shape)
+    wide = []
+    for seed in (9, 10):
+        g = f32(np.random.default_rng(seed).standard_normal(G) * 3.0)
+        net = ref_nn.NeuralNetwork(nodes=shape, weights=list(g), bias=True)
+        xr = np.random.default_rng(seed + 100)
+        for _ in range(16):
+            x = [float(v) for v in xr.integers(0, 321, size=6) / 320.0]
+            try:
+                net.run(x)
+            except Exception:
+                pass
+            a = np.array(net.list_of_transitional_arrays[-1][:-1], dtype=np.float64)
+            wide.append(dict(seed=seed, sigma=3.0, x=x, act=a.tolist(), idx=int(np.argmax(a)),
+                             genes_sha256=hashlib.sha256(g.tobytes()).hexdigest()))
+    with open(os.path.join(HERE, "nn_forward_wide_s3.json"), "w") as fh:
+        json.dump(wide, fh, indent=1)
+
+
 def gen_evaluate():
     """Whole evaluate(individual) (main.py:28-66) incl. the hall-of-fame shuffles."""
     cases = []
@@ -540,3 +640,7 @@ if __name__ == "__main__":
         gen_episodes()
     if "evaluate" in which:
         gen_evaluate()
+    if "episodes_s3" in which:
+        gen_episodes_s3()
+    if "wide_s3" in which:
+        gen_wide_s3()

@@ -38,11 +38,13 @@ def test_forward_matches_reference_golden(gpu, golden, key, precision):
     np.testing.assert_allclose(act.cpu().numpy(), g[f"{key}__act"], rtol=0, atol=tol)
 
 
-def test_forward_wide_golden(gpu, golden):
-    """[6,512,512,3] (config 5 shape) through the general f64 path."""
+@pytest.mark.parametrize("name", ["nn_forward_wide.json", "nn_forward_wide_s3.json"])
+def test_forward_wide_golden(gpu, golden, name):
+    """[6,512,512,3] (config 5 shape) through the general f64 path; σ 0.05 / 1
+    and the wide bench's σ 3 (_s3)."""
     from pong_amd.device import Evaluator
     import hashlib
-    cases = golden("nn_forward_wide.json")
+    cases = golden(name)
     shape = [6, 512, 512, 3]
     ev = Evaluator(shape, device=gpu, precision="f64")
     for c in cases:
@@ -254,13 +256,18 @@ def test_eval_edge_cases(gpu, oracle):
                     opponents=torch.zeros((2, G), dtype=torch.float64, device=gpu))
 
 
-def test_episode_traces_match_reference(gpu, golden):
-    """Per-frame actions of the REAL perform_episode (tests/golden/episodes.json)."""
+@pytest.mark.parametrize("name", ["episodes.json", "episodes_s3.json"])
+@pytest.mark.parametrize("kernel", ["auto", "staged"])
+def test_episode_traces_match_reference(gpu, golden, name, kernel):
+    """Per-frame actions of the REAL perform_episode (tests/golden/episodes.json;
+    episodes_s3.json: N(0, 3) genes, every game slot, long rallies and
+    2 000-frame timeouts), traced; then untraced, where the kernels jump over
+    periodic rallies -- frames, scores and rewards must not change."""
     from pong_amd.device import Evaluator
-    eps = golden("episodes.json")
+    eps = golden(name)
     for ep in eps:
         shape = ep["shape"]
-        ev = Evaluator(shape, device=gpu, n_games=ep["game_index"] + 1)
+        ev = Evaluator(shape, device=gpu, n_games=ep["game_index"] + 1, kernel=kernel)
         G = _gene_count(shape)
         n_games = ep["game_index"] + 1
         kinds = np.zeros((1, n_games), np.int32)
@@ -281,6 +288,12 @@ def test_episode_traces_match_reference(gpu, golden):
         # the action env.step received at frame t+1 is the decision traced at frame t
         np.testing.assert_array_equal(tr[:-1] & 3, np.array(ep["right_actions"][1:]))
         np.testing.assert_array_equal((tr[:-1] >> 2) & 3, np.array(ep["left_actions"][1:]))
+        res2, _ = ev.evaluate(_dev_genomes(np.array([ep["right"]]), gpu), torch.tensor(kinds, device=gpu),
+                              torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
+                              opponents=_dev_genomes(opponents, gpu))
+        assert int(res2.frames[0, gi]) == ep["frames"]
+        assert int(res2.scores[0, gi, 0]) == ep["score1"] and int(res2.scores[0, gi, 1]) == ep["score2"]
+        assert float(res2.rewards[0, gi]) == ep["reward"]
 
 
 # ---------------------------------------------------------- full-size runs

@@ -1,5 +1,6 @@
 """k_staged (PG_KERNEL_STAGED, csrc/pg_staged.hip) against the oracle and the
-reference's own episode traces, and against k_service at full size.
+reference's own episode traces (test_gpu_parity.py::test_episode_traces_match_reference
+runs them with kernel="staged" too), and against k_service at full size.
 
 The staged kernel plays the same games as k_service with each frame split
 into an environment stage (one lane per game) and a network stage; every
@@ -67,32 +68,6 @@ def test_staged_near_saturation(gpu, oracle):
     assert c[4] > 0 and c[5] > 0 and c[6] > 0, c
     assert c[8] > 0, c
     assert c[2] + c[5] + c[6] <= c[4], c
-
-
-def test_staged_episode_traces_match_reference(gpu, golden):
-    """Per-frame actions of the REAL perform_episode (tests/golden/episodes.json)."""
-    from pong_amd.device import Evaluator
-    for ep in golden("episodes.json"):
-        shape = ep["shape"]
-        n_games = ep["game_index"] + 1
-        ev = Evaluator(shape, device=gpu, n_games=n_games, kernel="staged")
-        G = _gene_count(shape)
-        kinds = np.zeros((1, n_games), np.int32)
-        kinds[0, ep["game_index"]] = ep["kind"]
-        opp = np.zeros((1, n_games), np.int32)
-        mult = np.ones((1, n_games))
-        mult[0, ep["game_index"]] = ep["mult"]
-        opponents = np.array([ep["opp"]]) if ep["opp"] is not None else np.zeros((1, G))
-        cap = ep["frames"] + 1
-        res, trace = ev.evaluate(_dev_genomes(np.array([ep["right"]]), gpu), torch.tensor(kinds, device=gpu),
-                                 torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
-                                 opponents=_dev_genomes(opponents, gpu), trace_games=n_games, trace_cap=cap)
-        gi = ep["game_index"]
-        assert int(res.frames[0, gi]) == ep["frames"]
-        assert float(res.rewards[0, gi]) == ep["reward"]
-        tr = trace[gi, : ep["frames"]].cpu().numpy()
-        np.testing.assert_array_equal(tr[:-1] & 3, np.array(ep["right_actions"][1:]))
-        np.testing.assert_array_equal((tr[:-1] >> 2) & 3, np.array(ep["left_actions"][1:]))
 
 
 def test_staged_without_opponents_and_with_rows(gpu, oracle):

@@ -26,9 +26,16 @@ def _episodes():
         return json.load(fh)
 
 
-@pytest.mark.parametrize("i", range(0, 32, 3))
-def test_perform_episode_matches_reference_trace(i):
-    ep = _episodes()[i]
+def _episodes_s3():
+    with open(os.path.join(HERE, "golden", "episodes_s3.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.mark.parametrize("case", [("episodes.json", i) for i in range(0, 32, 3)] +
+                         [("episodes_s3.json", i) for i in (0, 3, 5)])
+def test_perform_episode_matches_reference_trace(case):
+    name, i = case
+    ep = (_episodes() if name == "episodes.json" else _episodes_s3())[i]
     shape, kind = ep["shape"], ep["kind"]
     right = NL.NumpyNet(shape, np.array(ep["right"]))
     left = (NL.NumpyNet(shape, np.array(ep["opp"])) if kind == O.OPP_NN

@@ -33,19 +33,21 @@ def test_nn_forward_matches_reference(oracle, golden, key):
         np.testing.assert_allclose(act, act_ref[s], rtol=1e-13, atol=1e-15)
 
 
-def test_nn_forward_wide_matches_reference(oracle, golden):
+@pytest.mark.parametrize("name", ["nn_forward_wide.json", "nn_forward_wide_s3.json"])
+def test_nn_forward_wide_matches_reference(oracle, golden, name):
     shape = [6, 512, 512, 3]
     G = sum((shape[i] + 1) * shape[i + 1] for i in range(3))
-    for c in golden("nn_forward_wide.json")[:2]:
+    for c in golden(name)[:2]:
         genes = (np.random.default_rng(c["seed"]).standard_normal(G) * c["sigma"]).astype(np.float32).astype(np.float64)
         idx, act = oracle.nn_run(genes, shape, np.array(c["x"]))
         assert idx == c["idx"]
         np.testing.assert_allclose(act, c["act"], rtol=1e-12, atol=1e-14)
 
 
-def test_episode_traces_match_reference(oracle, golden):
-    eps = golden("episodes.json")
-    assert len(eps) == 32
+@pytest.mark.parametrize("name", ["episodes.json", "episodes_s3.json"])
+def test_episode_traces_match_reference(oracle, golden, name):
+    eps = golden(name)
+    assert len(eps) == (32 if name == "episodes.json" else 24)
     for ep in eps:
         opp = None if ep["opp"] is None else np.array(ep["opp"])
         r = oracle.play_game(np.array(ep["right"]), ep["shape"], ep["kind"], opp, ep["mult"],
