@@ -27,7 +27,7 @@ Shims (all documented in DESIGN.md "Oracle"):
     ``fitness.valid/values`` (deap is absent).
 
 Usage:  python tests/golden/make_golden.py   (takes a few minutes)
-        python tests/golden/make_golden.py episodes_s3 wide_s3   (the round-2 additions)
+        python tests/golden/make_golden.py episodes_s3 wide_s3 evaluate_s3   (round-2 additions)
         python tests/golden/make_golden.py hard_cases gpurun_out/.../hard_cases.npz
         (nn_hard_cases.npz from a tools/harvest_hard.py run on the GPU)
 """
@@ -533,6 +533,26 @@ def gen_wide_s3():
         json.dump(wide, fh, indent=1)
 
 
+def gen_evaluate_s3():
+    """Whole evaluate() calls at the bench's gene scale: 6 [6,64,3] individuals
+    with N(0, 3) genes against a 5-member N(0, 3) hall of fame whose fitness
+    values include negative ones (right_score_multiplier < 0)."""
+    rng = np.random.default_rng(707)
+    shape, G = [6, 64, 3], gene_count([6, 64, 3])
+    inds = [rng.standard_normal(G) * 3.0 for _ in range(6)]
+    hof_genes = [rng.standard_normal(G) * 3.0 for _ in range(5)]
+    hof_fit = [float(v) for v in np.round(rng.uniform(-1.8, 1.2, size=5), 4)]
+    hof = _HoF([_Ind(list(g), f) for g, f in zip(hof_genes, hof_fit)])
+    ns = make_namespace(shape, hall_of_fame=hof)
+    random.seed(11)
+    fits = [float(ns["evaluate"](list(g))[0]) for g in inds]
+    case = dict(shape=shape, random_seed=11, individuals=[g.tolist() for g in inds],
+                hof_genes=[g.tolist() for g in hof_genes], hof_fitness=hof_fit, fitness=fits, games=[])
+    print(f"evaluate s3: fitness={fits}", flush=True)
+    with open(os.path.join(HERE, "evaluate_s3.json"), "w") as fh:
+        json.dump([case], fh)
+
+
 def gen_evaluate():
     """Whole evaluate(individual) (main.py:28-66) incl. the hall-of-fame shuffles."""
     cases = []
@@ -644,3 +664,5 @@ if __name__ == "__main__":
         gen_episodes_s3()
     if "wide_s3" in which:
         gen_wide_s3()
+    if "evaluate_s3" in which:
+        gen_evaluate_s3()

@@ -27,13 +27,14 @@ class _HoF:
 
 
 def test_toolbox_map_evaluate_matches_reference(gpu, golden):
-    """evaluate.json: fitness of the REAL evaluate() (incl. hall-of-fame games)."""
+    """evaluate.json / evaluate_s3.json: fitness of the REAL evaluate() (incl.
+    hall-of-fame games; _s3: N(0, 3) genes, negative hall-of-fame fitness)."""
     import ga
     import main
     import utils
     saved = (utils.NETWORK_SHAPE, main.hall_of_fame)
     try:
-        for case in golden("evaluate.json"):
+        for case in golden("evaluate.json") + golden("evaluate_s3.json"):
             utils.NETWORK_SHAPE = case["shape"]
             main.hall_of_fame = _HoF([_Member(g, f) for g, f in zip(case["hof_genes"], case["hof_fitness"])])
             random.seed(case["random_seed"])
