@@ -486,16 +486,26 @@ __host__ __device__ constexpr int svc_threads() {
 // of (network, features), so a hit is exact.  Cleared at every game start.
 constexpr int kMemo = 8;
 
+// Relaxed workgroup-scope atomics on LDS words that another wave polls.  Not
+// `volatile`: a volatile access through the generic pointer of a __shared__
+// variable is not rewritten to LDS and becomes a flat access (sc0 sc1, a trip
+// through the vector-memory pipe, and a wait on every outstanding global load
+// and store of the wave).
+__device__ __forceinline__ int lds_ld(int *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st(int *a, int v) {
+  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 struct SlowSlot {
   const void *g;    // genome row of the network to re-decide
   int k[6];         // its doubled-centroid features
   float z[4];       // the f32 output pre-activations and their bound e
   float e;
   int idx;          // answer: argmax index
-  volatile int flag;  // 0 free, 1 posted, 2 answered
-  volatile int n_memo;  // decisions memoised for the current game's network
-  volatile uint64_t memo_key[kMemo];
-  volatile int memo_idx[kMemo];
+  int flag;  // 0 free, 1 posted, 2 answered (shared with the service wave: lds_ld / lds_st)
+  int n_memo;  // decisions memoised for the current game's network (the owning group only)
+  uint64_t memo_key[kMemo];
+  int memo_idx[kMemo];
   uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
   int rally_at, rally_span;
 };

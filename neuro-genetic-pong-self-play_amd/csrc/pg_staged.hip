@@ -122,15 +122,6 @@ struct StagedMemo {  // the network's last kMemo f64 decisions (as k_service's m
   int n;
 };
 
-// Relaxed workgroup-scope atomics on LDS words that another wave polls.  Not
-// `volatile`: a volatile access through the generic pointer of a __shared__
-// variable is not rewritten to LDS and becomes a flat access (sc0 sc1, and a
-// wait on every outstanding global load and store of the wave).
-__device__ __forceinline__ int lds_ld(int *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-__device__ __forceinline__ void lds_st(int *a, int v) {
-  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 constexpr int kStagedNetWaves = 7;
 constexpr int kStagedThreads = 64 * (kStagedNetWaves + 1);
 constexpr int kStagedLoads = 4;  // staging buffers: two game starts per frame x frame parity

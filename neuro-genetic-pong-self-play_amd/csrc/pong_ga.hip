@@ -34,6 +34,7 @@
 #include "pg_eval.hpp"
 #include "pg_f64math.h"
 #include "pg_cascade.hpp"
+#include "pg_service.hpp"
 
 #ifndef PG_VERSION_STRING
 #define PG_VERSION_STRING "pong_ga 0.1.0 (gfx950)"
@@ -278,286 +279,6 @@ __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
   }
 }
 
-
-template <int L, int U, int O, typename WT>
-__global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
-  constexpr int kSvcThreads = svc_threads<U>();
-  constexpr int kSvcGameWaves = kSvcThreads / 64 - 1;
-  constexpr int HL = L / 2;
-  constexpr int kSlots = kSvcGameWaves * (64 / L) * 2;
-  __shared__ SlowSlot slots[kSlots];
-  __shared__ int waves_done;
-  extern __shared__ double lds_svc[];  // f64_lds_doubles(H, O), service wave only
-  const int H = p.nodes[1];
-  const int b = p.bias;
-  const int wave = threadIdx.x >> 6;
-  const int lane64 = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < kSlots; i += kSvcThreads) slots[i].flag = 0;
-  if (threadIdx.x == 0) waves_done = 0;
-  __syncthreads();
-
-  if (wave == kSvcGameWaves) {
-    // ---------------- service wave: f64 re-decisions for the whole block ----
-    for (;;) {
-      bool served = false;
-      for (int base = 0; base < kSlots; base += 64) {
-        const int sidx = base + lane64;
-        const bool posted = sidx < kSlots && slots[sidx].flag == 1;
-        unsigned long long mask = __ballot(posted);
-        while (mask) {
-          const int sl = base + __builtin_ctzll(mask);
-          mask &= mask - 1;
-          __threadfence_block();
-          const WT *g = (const WT *)slots[sl].g;
-          int k[6];
-#pragma unroll
-          for (int i = 0; i < 6; ++i) k[i] = slots[sl].k[i];
-          float zf[O];
-#pragma unroll
-          for (int o = 0; o < O; ++o) zf[o] = slots[sl].z[o];
-          int idx = plateau_decide<O>(zf, slots[sl].e, lane64);
-          if (idx < 0) idx = fast_f64_decide<O, WT>(g, H, b, k, lane64);
-          // bit 8 / bit 9 of the answer: decided by the numpy-order forward / by the certified one
-          if (idx < 0) {
-            idx = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64);
-            if (p.hard_log && lane64 == 0) {
-              const long oo = g - (const WT *)p.opponents;
-              const bool opp = p.opponents != p.genomes && oo >= 0 && oo < (long)p.n_opponents * p.ostride;
-              log_hard(p, (int)(opp ? oo / p.ostride : (g - (const WT *)p.genomes) / p.gstride), opp ? 1 : 0,
-                       idx, 0, k);
-            }
-            idx |= 256;
-          } else {
-            idx |= 512;
-          }
-          if (lane64 == 0) {
-            slots[sl].idx = idx;
-            __threadfence_block();
-            slots[sl].flag = 2;
-          }
-          served = true;
-        }
-      }
-      if (!served) {
-        if (*(volatile int *)&waves_done == kSvcGameWaves) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    return;
-  }
-
-  // ---------------- game waves: k_split's loop --------------------------------
-  const int lig = threadIdx.x & (L - 1);
-  const int side = lig >= HL ? 1 : 0;  // 0: right paddle's network, 1: left paddle's
-  const int hl = lig & (HL - 1);
-  const int leader = lane64 & ~(L - 1);
-  // index (not a pointer) into the __shared__ array keeps every mailbox access
-  // a ds_* instruction; a SlowSlot * decays to a flat pointer
-  const int sx = (threadIdx.x / L) * 2 + side;
-  const WT *genomes = (const WT *)p.genomes;
-  const WT *opponents = (const WT *)p.opponents;
-
-  NetP<U, O> net;
-  Pong st;
-  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
-  const WT *gm = genomes;
-  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0;
-
-  const int games_total = active_total(p);
-  int w;
-  {
-    int ww = 0;
-    if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
-    w = group_broadcast<L>(ww, leader);
-  }
-  bool fresh = true;
-#ifdef PG_TIMELINE
-  uint64_t t_start = 0;
-  uint32_t g_fails = 0, g_slow = 0;
-#endif
-  while (w < games_total) {
-    if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
-      const int i = w / p.n_games;
-      const int g = w - i * p.n_games;
-      kind = p.kind[w];
-      const WT *gr = genomes + (long)genome_row(p, i) * p.gstride;
-      gm = (side && kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
-      load_net_pk<HL, U, O, WT>(net, gm, H, b, hl, side);  // the left network with the x-flip folded in
-      st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
-      act_r = act_l = timeout = total = frames = 0;
-      fresh = false;
-      if (hl == 0) slots[sx].n_memo = 0;
-#ifdef PG_TIMELINE  // experiment build: per-game wall-clock start/end into p.trace
-      t_start = wall_clock64();
-      g_fails = g_slow = 0;
-#endif
-    }
-    const int s1b = st.s1, s2b = st.s2;
-    const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
-    st.step(act_r, act_l);
-    frames += 1;
-    const int vis = st.vis;
-    const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
-    const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
-    int left = 0, right = 0;
-    if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
-      const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
-      // [bx, by, lbx, lby, me = right, enemy = left] for both halves: the left
-      // network's x-flip and me/enemy swap (main.py:146-147) are in its weights
-      const int k[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
-      float acc[O], z[O];
-      partial_pk<U, O>(net, k, acc);
-#pragma unroll
-      for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
-      int idx = certify<O>(z, net.e);
-      const bool left_nn = kind == kOppNN;
-      if (side && !left_nn) idx = 0;  // the left half is idle against a scripted opponent
-#ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
-      if (idx < 0) idx = z[1] > z[0] ? 1 : 0;
-#endif
-      if (idx < 0) {  // rare, half-uniform: the memo, else ask the service wave
-        fails += 1;
-#ifdef PG_TIMELINE
-        g_fails += 1;
-#endif
-        idx = plateau_f32<O>(z, net.e);
-        inwave += idx >= 0 ? 1 : 0;
-      }
-      if (idx < 0) {
-        const uint64_t key = memo_key(k);
-        const int nm = slots[sx].n_memo;
-        int hit = -1;
-#pragma unroll 1
-        for (int c = 0; c < kMemo && c < nm; ++c)
-          if (slots[sx].memo_key[c] == key) hit = slots[sx].memo_idx[c];
-        if (hit != -1) {
-          idx = hit;
-        } else {
-          if (hl == 0) {
-            // the network's own features (x-flipped for the left paddle): the f64 path uses the genes
-            const int kn[6] = {side ? 320 - bx2 : bx2, by2, side ? 320 - lbx2 : lbx2, lby2, side ? lc2 : rc2,
-                               side ? rc2 : lc2};
-            slots[sx].g = gm;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) slots[sx].k[i] = kn[i];
-#pragma unroll
-            for (int o = 0; o < O; ++o) slots[sx].z[o] = z[o];
-            slots[sx].e = net.e;
-            __threadfence_block();
-            slots[sx].flag = 1;
-          }
-          while (slots[sx].flag != 2) __builtin_amdgcn_s_sleep(1);
-          __threadfence_block();
-          const int ans = slots[sx].idx;
-          slow += (ans >> 8) & 1;
-#ifdef PG_TIMELINE
-          g_slow += 1;  // service round trips
-#endif
-          plateau += ans >> 9;
-          idx = ans & 255;
-          if (hl == 0) {
-            const int c = nm % kMemo;  // round-robin replacement
-            slots[sx].memo_key[c] = key;
-            slots[sx].memo_idx[c] = idx;
-            slots[sx].n_memo = nm + 1;
-            slots[sx].flag = 0;
-          }
-        }
-      }
-      const int mine = index_to_code(idx);
-      const int other = other_half<L>(mine);
-      right = side ? other : mine;
-      if (left_nn) {
-        left = side ? mine : other;
-      } else {  // HardcodedAi / ScoreHardcodedAi (dumb_ais.py), group-uniform: skipped in self-play
-        left = hardcoded(by2, lc2);
-        if (kind == kOppScore && st.s1 > st.s2) left = 0;
-      }
-      c_fwd += left_nn ? 2 : 1;
-    }
-    act_l = clamp_action(lc2, left);
-    act_r = clamp_action(rc2, right);
-#ifndef PG_TIMELINE
-    if (p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
-      if (w < p.trace_games && frames <= p.trace_cap && lig == 0)
-        p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
-    }
-#endif
-    if (frames > 1) {
-      if (st.s1 == s1b && st.s2 == s2b) {
-        timeout += 1;
-      } else {
-        total += timeout;
-        timeout = 0;
-      }
-    }
-#ifndef PG_NO_RALLY_SKIP
-    // a periodic rally ends at the timeout with nothing else changed: jump there
-    // (never while tracing, which records every frame's actions)
-#ifdef PG_TIMELINE
-    constexpr bool kTracing = false;  // the timeline build's trace buffer holds stamps, not actions
-#else
-    const bool kTracing = p.trace != nullptr;
-#endif
-    if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
-        !kTracing) {
-      const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
-      const uint64_t key = rally_key(st, act_r, act_l);
-      if (timeout == kRallyStart) {
-        if (lig == 0) {
-          slots[rs].rally_key = key;
-          slots[rs].rally_at = timeout;
-          slots[rs].rally_span = kRallyStart;
-        }
-      } else if (slots[rs].rally_key == key) {
-        const int rest = kTimeoutThresh + 1 - timeout;
-        frames += rest;
-        skipped += rest;
-        timeout = kTimeoutThresh + 1;
-      } else if (timeout - slots[rs].rally_at == slots[rs].rally_span) {
-        if (lig == 0) {
-          slots[rs].rally_key = key;
-          slots[rs].rally_at = timeout;
-          slots[rs].rally_span = 2 * slots[rs].rally_span;
-        }
-      }
-    }
-#endif
-    if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
-      if (lig == 0) finish_game(p, w, st, frames, total);
-#ifdef PG_TIMELINE
-      if (p.trace && w < p.trace_games && lig == 0) {
-        uint32_t *tl = (uint32_t *)(p.trace + (long)w * p.trace_cap);
-        tl[0] = (uint32_t)t_start;
-        tl[1] = (uint32_t)wall_clock64();
-        tl[2] = g_fails;
-        tl[3] = g_slow;
-      }
-#endif
-      c_steps += frames;
-      c_games += 1;
-      int ww = 0;
-      if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
-      w = group_broadcast<L>(ww, leader);
-      fresh = true;
-    }
-  }
-  if (p.counters && c_games) {
-    if (lig == 0) {
-      // env steps simulated: the episodes' frames minus those a periodic rally skipped
-      atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)(c_steps - skipped));
-      atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
-      atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
-      if (skipped) atomicAdd((unsigned long long *)&p.counters[8], (unsigned long long)skipped);
-    }
-    if (hl == 0 && slow) atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
-    if (hl == 0 && fails) atomicAdd((unsigned long long *)&p.counters[4], (unsigned long long)fails);
-    if (hl == 0 && plateau) atomicAdd((unsigned long long *)&p.counters[5], (unsigned long long)plateau);
-    if (hl == 0 && inwave) atomicAdd((unsigned long long *)&p.counters[6], (unsigned long long)inwave);
-  }
-  // this wave will post no more requests
-  if (lane64 == 0) atomicAdd(&waves_done, 1);
-}
 
 // --------------------------------------------------------------- decide ----
 // k_service's decision cascade on given inputs (pg_decide): the split layout's
@@ -1058,37 +779,26 @@ static int choose_split_lanes(int H) {
   return 64;
 }
 
-template <int L, int U, int O, typename WT>
-static int32_t launch_service(const EvalParams &p, hipStream_t s) {
-  constexpr int kSvcThreads = svc_threads<U>();
-  constexpr int GPB = (kSvcThreads / 64 - 1) * (64 / L);  // game groups per block
-  const size_t lds = (size_t)f64_lds_doubles(p.nodes[1], O) * sizeof(double);
-  const int want = (p.total + GPB - 1) / GPB;
-  const int cap = num_cus() * 2;
-  const int grid = want < cap ? want : cap;
-  if (grid <= 0) return PG_OK;
-  hipLaunchKernelGGL((k_service<L, U, O, WT>), dim3(grid), dim3(kSvcThreads), lds, s, p);
-  PG_HIP(hipGetLastError());
-  return PG_OK;
-}
-
 template <typename WT>
 static int32_t launch_service_any(const EvalParams &p, int L, int O, hipStream_t s) {
   const int H = p.nodes[1];
-#define PG_SVC(LL, UU)                                                   \
-  if (L == LL && (LL / 2) * UU >= H) {                                   \
-    if (O == 2) return launch_service<LL, UU, 2, WT>(p, s);              \
-    if (O == 3) return launch_service<LL, UU, 3, WT>(p, s);              \
-    if (O == 4) return launch_service<LL, UU, 4, WT>(p, s);              \
+  // the bench layout here (H in (32, 64] with L = 8: U = 16 is the smallest
+  // that holds it); every other (L, U) in pg_service_more.hip
+#ifdef PG_DEV_MIN
+  const bool here = L == 8 && H <= 64;
+#else
+  const bool here = L == 8 && H > 32 && H <= 64;
+#endif
+  if (here) {
+    if (O == 2) return launch_service<8, 16, 2, WT>(p, s);
+    if (O == 3) return launch_service<8, 16, 3, WT>(p, s);
+    if (O == 4) return launch_service<8, 16, 4, WT>(p, s);
   }
 #ifdef PG_DEV_MIN  // variant builds for experiments (tools/build_variant.sh): the bench layout only
-  PG_SVC(8, 16)
-#else
-  PG_SVC(8, 1) PG_SVC(8, 2) PG_SVC(8, 4) PG_SVC(8, 8) PG_SVC(8, 16) PG_SVC(16, 1) PG_SVC(16, 2) PG_SVC(16, 4) PG_SVC(16, 8)
-  PG_SVC(32, 1) PG_SVC(32, 2) PG_SVC(32, 4) PG_SVC(32, 8) PG_SVC(64, 1) PG_SVC(64, 2) PG_SVC(64, 4) PG_SVC(64, 8)
-#endif
-#undef PG_SVC
   return fail(PG_ERR_UNSUPPORTED, "no service kernel for L=%d H=%d O=%d", L, H, O);
+#else
+  return launch_service_more(p, L, O, sizeof(WT) == 8, s);
+#endif
 }
 
 template <int L, int U, typename WT>
