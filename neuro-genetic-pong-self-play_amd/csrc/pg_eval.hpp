@@ -46,6 +46,8 @@ struct EvalParams {
   int trace_games, trace_cap;
   int nodes[PG_MAX_NODES];
   int n_nodes, bias, max_width;
+  void *wide_scratch;  // k_wide: the blocks' tile-major W2 copies (workspace)
+  int wide_w3_resident;  // k_wide: every network's W3 kept in LDS for the genome's games
 };
 
 // Genome blocks / games this launch plays (pg_eval_args.n_active).  Made
@@ -99,20 +101,25 @@ __device__ inline double feat64_flip(int k) { return (160.0 - __dmul_rn(0.5, (do
 int num_cus();
 
 // Append one hard-decision record (pg_eval_args.hard_log); counters[9] counts them all.
-__device__ inline void log_hard(const EvalParams &p, int row, int is_opp, int idx, int source, const int k[6]) {
-  if (!p.hard_log || !p.counters) return;
-  const unsigned long long r = atomicAdd((unsigned long long *)&p.counters[9], 1ull);
-  if (r >= (unsigned long long)p.hard_cap) return;
-  uint32_t *rec = p.hard_log + r * 8;
+__device__ inline void log_hard_raw(uint32_t *hard_log, uint64_t *counters, int hard_cap, int row, int is_opp, int idx,
+                                    int source, const int k[6]) {
+  if (!hard_log || !counters) return;
+  const unsigned long long r = atomicAdd((unsigned long long *)&counters[9], 1ull);
+  if (r >= (unsigned long long)hard_cap) return;
+  uint32_t *rec = hard_log + r * 8;
   rec[0] = (uint32_t)row;
   rec[1] = (uint32_t)(is_opp & 1) | ((uint32_t)(idx & 255) << 8) | ((uint32_t)(source & 255) << 16);
   for (int i = 0; i < 6; ++i) rec[2 + i] = (uint32_t)k[i];
+}
+__device__ inline void log_hard(const EvalParams &p, int row, int is_opp, int idx, int source, const int k[6]) {
+  log_hard_raw(p.hard_log, p.counters, p.hard_cap, row, is_opp, idx, source, k);
 }
 
 // [6, H1, H2, O] networks (two hidden layers, H1, H2 <= 512, O in 2..4,
 // n_games <= 8) on the weight-streaming kernel k_wide (pg_wide.hip).
 bool wide_shape_ok(const pg_net &n, int n_games);
-int32_t launch_wide(const EvalParams &p, int dtype, hipStream_t s);
+size_t wide_workspace_bytes(const pg_eval_args *a);
+int32_t launch_wide(const EvalParams &p, int dtype, void *scratch, hipStream_t s);
 
 // [6, H<=256, 2..4] networks on the two-stage kernel k_staged (pg_staged.hip):
 // its extra workspace (prepared lane records of every row) and the launch.

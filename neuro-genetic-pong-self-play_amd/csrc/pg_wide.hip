@@ -11,10 +11,13 @@
 //      scripted left paddles; the set of networks that must run this frame
 //      (ball visible: get_actions main.py:143-153) goes to LDS.
 //   B  layer 1, thread j = hidden unit j, every needed column.
-//   C  layer 2: W2 tiles of 512 rows x K columns (128 B per row) pass
-//      HBM -> registers -> LDS (two tiles in flight per block), thread t owns
-//      row t and accumulates its dot product in np.dot's order (four partial
-//      sums k mod 4, blas_dot); the genome's tile serves its six games' columns.
+//   C  layer 2: thread t owns row t of W2 and accumulates its dot product in
+//      np.dot's order (four partial sums k mod 4, blas_dot).  Each network's
+//      W2 was re-laid TILE-MAJOR into the block's scratch when the genome
+//      started (K columns x every row per tile, 16-B pieces row-interleaved),
+//      so a wave's load is 1 KB contiguous and line-aligned and goes straight
+//      to registers: no LDS staging, no barrier inside the layer; the
+//      genome's tile serves its six games' columns.
 //   D  layer 3: one thread per (column, output).
 //   E  wave 0: argmax, clamp, bookkeeping, termination, results.
 // Every dot product is np.dot's own operation sequence (numpy_nn.py:126-129:
@@ -30,25 +33,121 @@ namespace pg {
 constexpr int kWideThreads = 512;  // = max H2: one W2 row per thread
 constexpr int kWideMaxGames = 8;
 
-// W2 tile: 128 B of each of the 512 rows, at a 144 B pitch in LDS (16 lanes'
-// ds_read_b128 of their own rows hit 16 distinct 16-B bank groups).
-constexpr int kTileRowBytes = 128, kTilePitch = 144;
+// W2 tiles: 128 B (K = 128 / sizeof(WT) columns) of every row.
+constexpr int kTileRowBytes = 128;
 #ifndef PG_WIDE_DEPTH
 #define PG_WIDE_DEPTH 2
 #endif
-constexpr int kDepth = PG_WIDE_DEPTH;  // register sets in the W2 tile ring (2 and 3 measured equal)
+constexpr int kDepth = PG_WIDE_DEPTH;  // tiles in flight per wave (register sets of the ring)
+// Tile reloads: issued together after the tile's arithmetic (kBurst), so the
+// compiler's in-order vmcnt accounting sees tile s's loads followed only by
+// the other ring slots' (its waits then let the whole ring stay in flight);
+// or one per 16-B piece, interleaved with the arithmetic (-DPG_WIDE_SPREAD).
+#ifdef PG_WIDE_SPREAD
+constexpr bool kBurst = false;
+#else
+constexpr bool kBurst = true;
+#endif
+// A scheduling fence after each 16-B piece of a tile: the scheduler would
+// otherwise hoist the LDS reads of all 32 columns' activations to the top of
+// the tile and spill the partial sums.
+#ifndef PG_WIDE_NO_FENCE
+#define PG_WIDE_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define PG_WIDE_FENCE() do {} while (0)
+#endif
 
 // LDS carve (bytes): feats [NC][8] f64 | outputs [NC][4] f64 | control |
-// opponent rows | rally keys | h1 [C2][NC] f64 | tile [512][144 B], reused for
-// h2 [C3][NC] f64 after layer 2.
+// opponent rows | rally keys | h1 [C2][NC] f64 (W3 staging after layer 2) |
+// h2 [C3][NC] f64 | when they fit: every network's W3 [NG + 1][O][C3] WT.
 constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffRally = 2048, kOffH1 = 2304;
 __host__ __device__ constexpr int align16(int v) { return (v + 15) & ~15; }
 
 __host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b) {
-  const int h1 = align16((H1 + b) * NC * 8);
-  const int tile = kWideThreads * kTilePitch;
-  const int h2 = align16((H2 + b) * NC * 8);
-  return kOffH1 + h1 + (tile > h2 ? tile : h2);
+  return kOffH1 + align16((H1 + b) * NC * 8) + align16((H2 + b) * NC * 8);
+}
+
+// The tile-major copy of one network's W2 in a block's scratch (written at
+// genome start by wide_prep, read once per frame by layer 2):
+//   tile s < T, piece q < 8, row r < RP: 16 B (E = 16 / sizeof(WT) weights,
+//   columns s*K + q*E ..) at ((s * 8 + q) * RP + r) * 16;
+//   then the tail (columns m2 .. C2-1, at most 3) of row r at (T * 8 * RP + r) * 16
+//   (a second such piece block for f64 weights).
+// m2 = C2 - C2 % 4 (blas_dot's block), T = max(1, ceil(m2 / K)), RP = H2 rounded up to 64.
+struct WideLayout {
+  int T, RP;
+  long net_bytes;
+};
+__host__ __device__ inline WideLayout wide_layout(int H1, int H2, int b, int wt_bytes) {
+  const int C2 = H1 + b, m2 = C2 - (C2 & 3), K = kTileRowBytes / wt_bytes;
+  WideLayout l;
+  l.T = m2 > K ? (m2 + K - 1) / K : 1;
+  l.RP = (H2 + 63) & ~63;
+  l.net_bytes = (long)(l.T * 8 + (3 * wt_bytes + 15) / 16) * l.RP * 16;
+  return l;
+}
+
+// Re-lay the W2 of each network in `need` (bit 0: the genome, bit 1 + c: game
+// c's opponent) tile-major into the block's scratch (WideLayout), and copy
+// the networks' W3 into LDS when it stays resident.  Thread t
+// copies row t, one tile (8 pieces) per batch of loads; consecutive threads
+// write consecutive 16 B, so a wave's store is 1 KB contiguous.  Once per
+// genome: about 1 % of the weight bytes the genome's frames stream.
+template <int NG, typename WT>
+__device__ void wide_prep(unsigned char *scratch, const WideLayout lay, const WT *gw2, const WT *ow2,
+                          const long long *orow, unsigned need, int C2, int H2, int t, WT *w3r, int n_w3,
+                          long w3_off) {
+  // W3 (n_w3 = O * C3 weights, w3_off elements after W2's start) of every
+  // needed network into LDS for the genome's games (w3r: the LDS copy, or NULL)
+  if (w3r) {
+    for (int n = 0; n <= NG; ++n) {
+      if (!((need >> n) & 1)) continue;
+      const WT *src = (n == 0 ? gw2 : ow2 + orow[n - 1]) + w3_off;
+      for (int i = t; i < n_w3; i += kWideThreads) w3r[n * n_w3 + i] = src[i];
+    }
+  }
+  constexpr int E = 16 / (int)sizeof(WT), kTP = (3 * (int)sizeof(WT) + 15) / 16;
+  const int m3 = C2 & 3, m2 = C2 - m3;
+  const long PB = (long)lay.RP * 16;
+  for (int n = 0; n <= NG; ++n) {
+    if (!((need >> n) & 1) || t >= H2) continue;
+    const WT *row = (n == 0 ? gw2 : ow2 + orow[n - 1]) + (long)t * C2;
+    unsigned char *dst = scratch + (long)n * lay.net_bytes + t * 16;
+    for (int s = 0; s < lay.T; ++s) {
+      WT v[8][E];
+      const int k0 = s * 8 * E;
+      if (k0 + 8 * E <= m2) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+          for (int e = 0; e < E; ++e) v[q][e] = row[k0 + q * E + e];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+          for (int e = 0; e < E; ++e) v[q][e] = k0 + q * E + e < m2 ? row[k0 + q * E + e] : WT(0);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint4 u;
+        __builtin_memcpy(&u, v[q], 16);
+        *(uint4 *)(dst + (s * 8 + q) * PB) = u;
+      }
+    }
+    WT tv[kTP * E];
+#pragma unroll
+    for (int i = 0; i < kTP * E; ++i) tv[i] = i < m3 ? row[m2 + i] : WT(0);
+#pragma unroll
+    for (int i = 0; i < kTP; ++i) {
+      uint4 u;
+      __builtin_memcpy(&u, tv + i * E, 16);
+      *(uint4 *)(dst + (lay.T * 8 + i) * PB) = u;
+    }
+  }
+  // the copies are read back through the vector caches by other waves of the block
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // numpy's sigmoid, out of line: one copy of the libm pow instead of one per
@@ -79,20 +178,25 @@ __device__ __forceinline__ bool near_tie(const double *v, int O) {
   }
   return t1 - t2 <= 1e-12 && !(t2 == 1.0);
 }
-__device__ __noinline__ void log_wide(const EvalParams &p, int row, int is_opp, int idx, const double *x) {
+// (the fields, not the EvalParams: a reference to the kernel's parameter
+// block makes the compiler copy it to private memory, and every field read
+// from there counts as divergent -- layer 2's buffer descriptors included)
+__device__ __noinline__ void log_wide(uint32_t *hard_log, uint64_t *counters, int hard_cap, int row, int is_opp,
+                                      int idx, const double *x) {
   int k[6];
   for (int i = 0; i < 6; ++i) k[i] = (int)rint(x[i] * 320.0);  // the doubled centroids back from k/320
-  log_hard(p, row, is_opp, idx, 1, k);
+  log_hard_raw(hard_log, counters, hard_cap, row, is_opp, idx, 1, k);
 }
 
 // Diagnostic build (-DPG_WIDE_STAMPS): thread 0 adds the shader-clock cycles
-// between the frame's phase boundaries into counters[4..6] (A+E+B, C, D).
+// between phase boundaries into counters[4] (E + A), [5] (B), [6] (C),
+// [10] (D) and [11] (a genome's prep: tile-major W2 copies, W3 to LDS).
 #ifdef PG_WIDE_STAMPS
 #define PG_STAMP(i)                                                        \
   do {                                                                     \
     if (t == 0) {                                                          \
       const uint64_t now_ = __builtin_amdgcn_s_memtime();                  \
-      stamp_acc[(i) == 0 ? 0 : (i) == 1 ? 0 : (i) == 2 ? 1 : 2] += now_ - stamp_last; \
+      stamp_acc[i] += now_ - stamp_last;                                   \
       stamp_last = now_;                                                   \
     }                                                                      \
   } while (0)
@@ -105,17 +209,19 @@ __device__ __noinline__ void log_wide(const EvalParams &p, int row, int is_opp, 
 template <int NG, typename WT>
 __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
 #ifdef PG_WIDE_STAMPS
-  uint64_t stamp_acc[3] = {0, 0, 0}, stamp_last = __builtin_amdgcn_s_memtime();
+  uint64_t stamp_acc[5] = {0, 0, 0, 0, 0}, stamp_last = __builtin_amdgcn_s_memtime();
 #endif
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int NC = 2 * NG;  // columns: right (genome) of game c = c, left (opponent) of game c = NG + c
   constexpr int K = kTileRowBytes / (int)sizeof(WT);
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  // wid through readfirstlane: the compiler then knows it (and whatever depends
+  // on it only) is wave-uniform, so layer 2's buffer descriptors and scalar
+  // offsets stay in SGPRs instead of a per-load waterfall loop
+  const int t = threadIdx.x, lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int b = p.bias;
   const int H1 = p.nodes[1], H2 = p.nodes[2], O = p.nodes[3];
   const int C1 = 6 + b, C2 = H1 + b, C3 = H2 + b;
   const long W1n = (long)H1 * C1, W2n = (long)H2 * C2;
-  const int T = (C2 + K - 1) / K;  // tiles per W2
 
   double *feat = (double *)lds_raw;              // [NC][8]
   double *outv = (double *)(lds_raw + kOffOut);  // [NC][4]
@@ -124,8 +230,13 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   uint64_t *rkey = (uint64_t *)(lds_raw + kOffRally);    // [NG] Brent's saved rally key per game
   int *rat = (int *)(lds_raw + kOffRally + 64), *rspan = (int *)(lds_raw + kOffRally + 96);
   double *h1 = (double *)(lds_raw + kOffH1);            // [C2][NC]
-  unsigned char *tile = lds_raw + kOffH1 + align16(C2 * NC * 8);
-  double *h2 = (double *)tile;  // [C3][NC], after layer 2
+  double *h2 = (double *)(lds_raw + kOffH1 + align16(C2 * NC * 8));  // [C3][NC]
+  const WideLayout lay = wide_layout(H1, H2, b, (int)sizeof(WT));
+  const int m3 = C2 & 3, m2 = C2 - m3;
+  // this block's tile-major W2 copies: net 0 = the genome, 1 + c = game c's opponent
+  unsigned char *scratch = (unsigned char *)p.wide_scratch + (long)blockIdx.x * (NG + 1) * lay.net_bytes;
+  // [NG + 1][O][C3] W3 copies after the h2 region, or NULL (staged per frame)
+  WT *w3r = p.wide_w3_resident ? (WT *)(lds_raw + wide_lds_bytes(NC, H1, H2, b)) : nullptr;
 
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
@@ -136,7 +247,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   for (;;) {  // genomes, one per workgroup at a time
     if (t == 0) ctl[0] = (int)atomicAdd(p.work, 1u);
     __syncthreads();
-    const int gi = ctl[0];
+    const int gi = __builtin_amdgcn_readfirstlane(ctl[0]);  // uniform: the genome loop's exit
     if (gi >= n_genomes_active) break;
     const int grow = genome_row(p, gi);
     const WT *gbase = genomes + (long)grow * p.gstride;
@@ -152,6 +263,13 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       st.reset(game_seed(p.seed, lane), kind == kOppRomCpu);
       active = true;
     }
+    if (wid == 0) {
+      const uint64_t nb = __ballot(lane < n_games && kind == kOppNN);
+      if (lane == 0) ctl[1] = 1 | (int)((unsigned)nb << 1);  // networks to re-lay: bit 0 genome, 1 + c opponents
+    }
+    __syncthreads();
+    wide_prep<NG, WT>(scratch, lay, gbase + W1n, opponents + W1n, orow, ctl[1], C2, H2, t, w3r, O * C3, W2n);
+    PG_STAMP(4);
     for (int fno = 0;; ++fno) {  // frames, all games in lockstep
       int *cf = ctl + 8 + (fno & 1) * 32;  // [0] column mask, [1] any active, [2] nets, [3..] net ids
       // ---- A: env.step + find_stuff + inference features (main.py:77-87)
@@ -198,100 +316,127 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       }
       __syncthreads();
       PG_STAMP(0);
-      const unsigned mask = (unsigned)cf[0];
-      if (!cf[1]) break;
-      const int n_nets = cf[2];
+      // LDS loads count as divergent: readfirstlane makes the frame's control words uniform
+      const unsigned mask = (unsigned)__builtin_amdgcn_readfirstlane(cf[0]);
+      if (!__builtin_amdgcn_readfirstlane(cf[1])) break;
+      const int n_nets = __builtin_amdgcn_readfirstlane(cf[2]);
       c_streams += n_nets;  // uniform: every thread counts, thread 0 reports
 
       if (mask) {
-        // ---- B: layer 1, h1 = S(W1 . [x; 1]) per needed column (numpy_nn.py:126-129)
-        for (int j = t; j < H1; j += kWideThreads) {
-          if (mask & ((1u << NG) - 1)) {
-            const WT *row = gbase + (long)j * C1;
-            double wv[7];
+        // layer 2's streaming setup and its first kDepth tiles
+        constexpr int kTP = (3 * (int)sizeof(WT) + 15) / 16;  // tail pieces per row
+        const int T = lay.T;
+        const int S = n_nets * T;
+        const int PB = lay.RP * 16;  // bytes of one piece of every row
+        // Steps s >= S load through an empty descriptor (no memory traffic), so
+        // every issue is unconditional and the waits stay counted; a tail
+        // piece is fetched only with a network's last tile (out-of-range
+        // offset otherwise).
+        struct Src {
+          __amdgpu_buffer_rsrc_t rsrc;
+          int soff;
+          uint32_t toff;
+        };
+        auto source = [&](int s) -> Src {
+          const bool valid = s < S;
+          const int net = valid ? __builtin_amdgcn_readfirstlane(cf[3 + s / T]) : 0;
+          const int tl = valid ? s % T : 0;
+          const uint64_t ad = (uint64_t)(scratch + (long)net * lay.net_bytes);
+          const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ad);
+          const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32));
+          Src r;
+          r.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                                     valid ? (int)lay.net_bytes : 0, 0x00020000);
+          r.soff = tl * 8 * PB;
+          r.toff = (valid && tl == T - 1) ? (uint32_t)(T * 8 * PB + t * 16) : 0x80000000u;
+          return r;
+        };
+        auto load = [&](const Src &src, int q) -> uint4 {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, t * 16, src.soff + q * PB, 0);
+          return make_uint4(v[0], v[1], v[2], v[3]);
+        };
+        auto load_tail = [&](const Src &src, uint4 (&rt)[kTP]) {
 #pragma unroll
-            for (int i = 0; i < 7; ++i) wv[i] = (i < C1) ? (double)row[i] : 0.0;
+          for (int i = 0; i < kTP; ++i) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, src.toff + i * PB, 0, 0);
+            rt[i] = make_uint4(v[0], v[1], v[2], v[3]);
+          }
+        };
+        const bool stream_rows = wid * 64 < H2;  // wave-uniform: a wave past the last row streams nothing
+        uint4 R[kDepth][8], RT[kDepth][kTP];
+        auto prologue = [&]() {
+          if (stream_rows) {
 #pragma unroll
-            for (int c = 0; c < NG; ++c) {
-              if (!((mask >> c) & 1)) continue;
-              const double *x = feat + c * 8;
-              h1[j * NC + c] = sigmoid_f64_call(blas_dot6(wv, x, b));
+            for (int d = 0; d < kDepth; ++d) {
+              const Src src = source(d);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) R[d][q] = load(src, q);
+              load_tail(src, RT[d]);
             }
           }
+        };
+#ifndef PG_WIDE_LATE_PROLOGUE
+        prologue();
+#endif
+
+        // ---- B: layer 1, h1 = S(W1 . [x; 1]) per needed column (numpy_nn.py:126-129),
+        // thread j = unit j (H1 <= 512), after the frame's first kDepth W2
+        // tiles were requested (layer 2 starts with them in flight).  Every
+        // needed network's W1 row j is requested at once, the pre-activations
+        // go to h1, then the inlined sigmoid runs over all columns, four at a
+        // time (unneeded columns compute garbage nobody reads; no call: the
+        // tiles in flight stay in VGPRs).
+        const int j = t;
+        WT w1[NG + 1][7];
+        if (j < H1) {
 #pragma unroll
-          for (int c = 0; c < NG; ++c) {
-            if (!((mask >> (NG + c)) & 1)) continue;
-            const WT *row = opponents + orow[c] + (long)j * C1;
-            const double *x = feat + (NG + c) * 8;
-            double wo[7];
+          for (int n = 0; n <= NG; ++n) {
+            const bool need = n == 0 ? (mask & ((1u << NG) - 1)) != 0 : ((mask >> (NG + n - 1)) & 1) != 0;
+            const WT *row = (n == 0 ? gbase : opponents + orow[n == 0 ? 0 : n - 1]) + (long)j * C1;
 #pragma unroll
-            for (int i = 0; i < 7; ++i) wo[i] = (i < C1) ? (double)row[i] : 0.0;
-            h1[j * NC + NG + c] = sigmoid_f64_call(blas_dot6(wo, x, b));
+            for (int i = 0; i < 7; ++i) w1[n][i] = (need && i < C1) ? row[i] : WT(0);
           }
+        }
+        if (j < H1) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            if (!((mask >> c) & 1)) continue;
+            double w[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) w[i] = (double)w1[c < NG ? 0 : 1 + c - NG][i];
+            h1[j * NC + c] = blas_dot6(w, feat + c * 8, b);
+          }
+#pragma unroll 4
+          for (int c = 0; c < NC; ++c) h1[j * NC + c] = sigmoid_f64(h1[j * NC + c]);
         }
         if (b && t < NC) h1[H1 * NC + t] = 1.0;
         __syncthreads();
         PG_STAMP(1);
 
-        // ---- C: layer 2, W2 streamed in tiles; thread t accumulates row t.
-        // A tile is 128 B of every row (K = 128 / sizeof(WT) columns); lane
-        // t loads 16 B pieces (chunk t % 8 of rows t / 8 + 64 it), so each
-        // wave-instruction reads 8 rows x 128 B.  Tiles pass through a ring
-        // of kDepth register sets: while tile s is multiplied out of LDS,
-        // tiles s+1 .. s+kDepth are in flight.
-        // Row sums in np.dot's order (pg_device.hpp blas_dot; C2 <= 513 is one
-        // block): four partial sums k mod 4 over k < m2 (kind 0: fused
-        // multiply-add; kind 1: two sums k mod 2; kind 2: rounded products),
-        // the m3 = C2 & 3 trailing weights kept for the tail after the last tile.
+        // ---- C: layer 2, W2 streamed tile by tile from the block's tile-major
+        // copies (wide_prep); thread t accumulates row t in np.dot's order
+        // (pg_device.hpp blas_dot; C2 <= 513 is one block): four partial sums
+        // k mod 4 over k < m2 (kind 0: fused multiply-add; kind 1: two sums
+        // k mod 2; kind 2: rounded products), then the m3 trailing weights (the
+        // layout's tail pieces, loaded with the network's last tile).  A wave's
+        // piece load is 1 KB contiguous (64 rows x 16 B) and goes straight to
+        // registers; tiles pass through a ring of kDepth register sets, the
+        // next tile's loads spread over the current tile's arithmetic, so each
+        // wave streams on its own -- no barrier until the layer is done.
         const int kind2 = blas_kind(t, H2);
-        const int m3 = C2 & 3, m2 = C2 - m3;
+        // wave-uniform: every row of this wave sums with fused multiply-adds
+        // (branches on the per-row kind would put the tile loads under
+        // divergent control flow)
+        const bool wave_k0 = wid * 64 + 64 <= 4 * (H2 >> 2);
         double zg[NG][4];  // the genome's partial sums (per game)
         double zp[4];      // the current opponent network's partial sums
-        double zop[NG];    // finished opponents' row sums (written once per network pass)
-        double tw[3] = {0.0, 0.0, 0.0};  // the current network's tail weights
-        double tg[3] = {0.0, 0.0, 0.0};  // the genome's tail weights
 #pragma unroll
         for (int c = 0; c < NG; ++c) {
-          zop[c] = 0.0;
 #pragma unroll
           for (int l = 0; l < 4; ++l) zg[c][l] = 0.0;
         }
 #pragma unroll
         for (int l = 0; l < 4; ++l) zp[l] = 0.0;
-        const int S = n_nets * T;
-        const int lane_off = (t >> 3) * C2 * (int)sizeof(WT) + (t & 7) * 16;
-        const int w2_bytes = H2 * C2 * (int)sizeof(WT);
-        // Steps s >= S load through an empty descriptor (no memory traffic), so
-        // every issue is unconditional and the waits stay counted.
-        // Tile s+kDepth's loads are spread over tile s's arithmetic (one
-        // 16-B piece per piece of work): a wave whose loads cannot all be
-        // accepted at once keeps computing instead of stalling at the issue.
-        struct Src {
-          __amdgpu_buffer_rsrc_t rsrc;
-          int k0;
-        };
-        auto source = [&](int s) -> Src {
-          const bool valid = s < S;
-          const int net = valid ? __builtin_amdgcn_readfirstlane(cf[3 + s / T]) : 0;
-          const int k0 = valid ? (s % T) * K : 0;
-          const WT *base = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n;
-          const uint64_t ad = (uint64_t)base;
-          const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ad);
-          const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32));
-          return {__builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
-                                                    valid ? w2_bytes : 0, 0x00020000),
-                  k0};
-        };
-        auto load = [&](const Src &src, int it) -> uint4 {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-              src.rsrc, lane_off, (src.k0 + it * 64 * C2) * (int)sizeof(WT), 0);
-          return make_uint4(v[0], v[1], v[2], v[3]);
-        };
-        auto store = [&](const uint4 (&r)[8]) {
-#pragma unroll
-          for (int it = 0; it < 8; ++it)
-            *(uint4 *)((unsigned char *)tile + (it * 64 + (t >> 3)) * kTilePitch + (t & 7) * 16) = r[it];
-        };
         // one weight wk at row position kk (kk % 4 == l) into partial sums a
         auto accum = [&](double (&a)[4], int l, double wk, double h) {
           if (kind2 == 0) {
@@ -305,29 +450,36 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             }
           }
         };
-        // multiply tile s (in LDS) into the row sums and load tile sn into r
-        auto compute = [&](int s, uint4 (&r)[8], int sn) {
+        // the tail weight i (< m3) out of the tail pieces
+        auto tail_w = [&](const uint4 (&rt)[kTP], int i) -> double {
+          WT tq[kTP * 16 / (int)sizeof(WT)];
+          __builtin_memcpy(tq, rt, sizeof(tq));
+          return (double)tq[i];
+        };
+        // multiply tile s (in r / rt) into the row sums and load tile sn into r / rt
+        auto compute = [&](int s, uint4 (&r)[8], uint4 (&rt)[kTP], int sn) {
           const Src src = source(sn);
-          bool work = s < S && t < H2;
+          // rows t >= H2 of a partial last wave sum garbage that is never stored
+          bool work = s < S;
 #ifdef PG_WIDE_NOCOMPUTE
           work = false;  // diagnostic build: streaming only
 #endif
           if (!work) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) r[q] = load(src, q);
+            load_tail(src, rt);
             return;
           }
-          const int net = cf[3 + s / T], tl = s % T, k0 = tl * K;
-          const int kn = min(K, C2 - k0);
-          const bool full = k0 + K <= m2;  // the whole tile is inside the block (no tail, no end)
-          const unsigned char *tr = (const unsigned char *)tile + t * kTilePitch;
+          const int net = __builtin_amdgcn_readfirstlane(cf[3 + s / T]), tl = s % T, k0 = tl * K;
+          const int kn = min(K, m2 - k0);  // this tile's weights inside the block
+          const bool full = kn == K;
           constexpr int E = 16 / (int)sizeof(WT);  // weights per 16-B piece
           if (net == 0) {
-            if (full && kind2 == 0) {  // the hot case: every element a fused multiply-add
+            if (full && wave_k0) {  // the hot case: every element a fused multiply-add
 #pragma unroll
               for (int q = 0; q < 8; ++q) {
-                const uint4 v = *(const uint4 *)(tr + q * 16);
-                r[q] = load(src, q);
+                const uint4 v = r[q];
+                if (!kBurst) r[q] = load(src, q);
                 WT wq[E];
                 __builtin_memcpy(wq, &v, 16);
 #pragma unroll
@@ -338,29 +490,33 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
 #pragma unroll
                   for (int c = 0; c < NG; ++c) zg[c][k & 3] = fma(wk, hp[c], zg[c][k & 3]);
                 }
+                PG_WIDE_FENCE();
               }
             } else {
 #pragma unroll
               for (int q = 0; q < 8; ++q) {
-                const uint4 v = *(const uint4 *)(tr + q * 16);
-                r[q] = load(src, q);
+                const uint4 v = r[q];
+                if (!kBurst) r[q] = load(src, q);
                 WT wq[E];
                 __builtin_memcpy(wq, &v, 16);
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                  const int k = q * E + e, kk = k0 + k;
+                  const int k = q * E + e;
                   if (k < kn) {
-                    const double wk = (double)wq[e];
-                    if (kk < m2) {
-                      const double *hp = h1 + kk * NC;
+                    const double *hp = h1 + (k0 + k) * NC;
 #pragma unroll
-                      for (int c = 0; c < NG; ++c) accum(zg[c], k & 3, wk, hp[c]);
-                    } else {
-#pragma unroll
-                      for (int i = 0; i < 3; ++i) tg[i] = (kk - m2 == i) ? wk : tg[i];
-                    }
+                    for (int c = 0; c < NG; ++c) accum(zg[c], k & 3, (double)wq[e], hp[c]);
                   }
                 }
+              }
+            }
+            if (tl == T - 1 && t < H2) {  // the genome's pass is complete: its row sums (pre-activations) to h2
+#pragma unroll
+              for (int c = 0; c < NG; ++c) {
+                const double y =
+                    __dadd_rn(0.0, __dadd_rn(__dadd_rn(zg[c][0], zg[c][2]), __dadd_rn(zg[c][1], zg[c][3])));
+                h2[t * NC + c] = blas_tail([&](int i) { return tail_w(rt, i - m2); },
+                                           [&](int i) { return h1[i * NC + c]; }, m2, m3, y);
               }
             }
           } else {
@@ -369,11 +525,11 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
 #pragma unroll
               for (int l = 0; l < 4; ++l) zp[l] = 0.0;
             }
-            if (full && kind2 == 0) {
+            if (full && wave_k0) {
 #pragma unroll
               for (int q = 0; q < 8; ++q) {
-                const uint4 v = *(const uint4 *)(tr + q * 16);
-                r[q] = load(src, q);
+                const uint4 v = r[q];
+                if (!kBurst) r[q] = load(src, q);
                 WT wq[E];
                 __builtin_memcpy(wq, &v, 16);
 #pragma unroll
@@ -381,118 +537,126 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
                   const int k = q * E + e;
                   zp[k & 3] = fma((double)wq[e], hp[(k0 + k) * NC], zp[k & 3]);
                 }
+                PG_WIDE_FENCE();
               }
             } else {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const uint4 v = *(const uint4 *)(tr + q * 16);
-              r[q] = load(src, q);
-              WT wq[E];
-              __builtin_memcpy(wq, &v, 16);
+              for (int q = 0; q < 8; ++q) {
+                const uint4 v = r[q];
+                if (!kBurst) r[q] = load(src, q);
+                WT wq[E];
+                __builtin_memcpy(wq, &v, 16);
 #pragma unroll
-              for (int e = 0; e < E; ++e) {
-                const int k = q * E + e, kk = k0 + k;
-                if (k < kn) {
-                  const double wk = (double)wq[e];
-                  if (kk < m2) {
-                    accum(zp, k & 3, wk, hp[kk * NC]);
-                  } else {
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) tw[i] = (kk - m2 == i) ? wk : tw[i];
-                  }
+                for (int e = 0; e < E; ++e) {
+                  const int k = q * E + e;
+                  if (k < kn) accum(zp, k & 3, (double)wq[e], hp[(k0 + k) * NC]);
                 }
               }
             }
-            }
-            if (tl == T - 1) {  // once per network pass: the block sum and the tail
+            if (tl == T - 1 && t < H2) {  // once per network pass: the block sum and the tail, to h2
               const double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(zp[0], zp[2]), __dadd_rn(zp[1], zp[3])));
-              zop[net - 1] =
-                  blas_tail([&](int i) { return tw[i - m2]; }, [&](int i) { return hp[i * NC]; }, m2, m3, y);
+              h2[t * NC + NG + net - 1] = blas_tail([&](int i) { return tail_w(rt, i - m2); }, [&](int i) { return hp[i * NC]; },
+                                       m2, m3, y);
             }
           }
+          if (kBurst) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) r[q] = load(src, q);
+          }
+          load_tail(src, rt);
         };
 
-        // ring: before step s, LDS holds tile s, set s % kDepth is free and
-        // sets (s+1 .. s+kDepth-1) % kDepth hold tiles in flight
-        uint4 R[kDepth][8];
+        // ring: before step s, set s % kDepth holds tile s and sets
+        // (s+1 .. s+kDepth-1) % kDepth hold tiles in flight
+#ifdef PG_WIDE_LATE_PROLOGUE
+        prologue();
+#endif
+        if (stream_rows) {
+          for (int s = 0; s < S; s += kDepth) {
 #pragma unroll
-        for (int d = 0; d < kDepth; ++d) {
-          const Src src = source(d);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) R[d][q] = load(src, q);
-        }
-        store(R[0]);
-        __syncthreads();
-        for (int s = 0; s < S; s += kDepth) {
-#pragma unroll
-          for (int d = 0; d < kDepth; ++d) {
-            compute(s + d, R[d], s + d + kDepth);
-            __syncthreads();
-            store(R[(d + 1) % kDepth]);  // tile s+d+1
-            __syncthreads();
+            for (int d = 0; d < kDepth; ++d) compute(s + d, R[d], RT[d], s + d + kDepth);
           }
         }
-        // every tile read is behind the last barrier: h2 may overwrite the tile
         if (t < H2) {
-          double zgf[NG];
-#pragma unroll
-          for (int c = 0; c < NG; ++c) {
-            const double y = __dadd_rn(0.0, __dadd_rn(__dadd_rn(zg[c][0], zg[c][2]), __dadd_rn(zg[c][1], zg[c][3])));
-            zgf[c] = blas_tail([&](int i) { return tg[i - m2]; }, [&](int i) { return h1[i * NC + c]; }, m2, m3, y);
-          }
-#pragma unroll
+#pragma unroll 4
           for (int c = 0; c < NC; ++c) {
-            const double zc = c < NG ? zgf[c] : zop[c - NG];
-            h2[t * NC + c] = ((mask >> c) & 1) ? sigmoid_f64_call(zc) : 0.0;
+            const double v = sigmoid_f64(h2[t * NC + c]);
+            h2[t * NC + c] = ((mask >> c) & 1) ? v : 0.0;
           }
         }
         if (b && t < NC) h2[H2 * NC + t] = 1.0;
         __syncthreads();
         PG_STAMP(2);
 
-        // ---- D: layer 3 + output sigmoid, one thread per (needed column, output).
-        // The needed networks' W3 rows are first staged into the h1 region
-        // (dead after layer 2) by all threads with coalesced loads, as many
-        // networks at a time as fit, so the sequential sums read only LDS.
+        // ---- D: layer 3 + output sigmoid (numpy_nn.py:126-131).  Four threads
+        // per (needed column, output): thread l of the quad runs np.dot's
+        // partial sum l (kinds 0, 2: i = l mod 4; kind 1: i = l mod 2, l < 2),
+        // the quad's first thread combines the sums in dgemv_t's order, adds
+        // the tail and takes the sigmoid -- blas_dot's operations exactly.
+        // W3 rows come from LDS: resident since the genome started (wide_prep)
+        // when they fit, else staged here into the h1 region (dead after
+        // layer 2) with coalesced loads, as many networks at a time as fit.
         {
-          WT *w3s = (WT *)h1;
-          const int per_net = O * C3;
-          const int cap = (C2 * NC * 8) / (per_net * (int)sizeof(WT));
-          const unsigned rbits = mask & ((1u << NG) - 1);
-          for (int g0 = 0; g0 < n_nets; g0 += cap) {
-            const int gn = min(cap, n_nets - g0);
-            // kW3Batch loads in flight per thread before any LDS store (a
-            // load-then-store loop waits out one HBM round trip per element)
-            constexpr int kW3Batch = 8;
-            for (int i0 = t; i0 < gn * per_net; i0 += kW3Batch * kWideThreads) {
-              WT val[kW3Batch];
-#pragma unroll
-              for (int q = 0; q < kW3Batch; ++q) {
-                const int i = i0 + q * kWideThreads;
-                const int ii = i < gn * per_net ? i : i0;
-                const int slot = ii / per_net, net = cf[3 + g0 + slot];
-                const WT *v = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n + W2n;
-                val[q] = v[ii - slot * per_net];
-              }
-#pragma unroll
-              for (int q = 0; q < kW3Batch; ++q)
-                if (i0 + q * kWideThreads < gn * per_net) w3s[i0 + q * kWideThreads] = val[q];
+          const int nq = __builtin_popcount(mask) * O;  // chains
+          const int m3o = C3 & 3, m2o = C3 - m3o;      // C3 <= 513: one block
+          const int qi = t >> 2, l = t & 3;
+          const int o = qi % O, c = qi < nq ? nth_set_bit(mask, qi / O) : 0;
+          const int kd = blas_kind(o, O);
+          const double *hp = h2 + c;
+          auto chain = [&](const WT *v) {  // v: W3 row o of column c's network
+            double sl = 0.0;
+            if (kd == 0) {
+#pragma unroll 8
+              for (int i = l; i < m2o; i += 4) sl = fma((double)v[i], hp[i * NC], sl);
+            } else if (kd == 2) {
+#pragma unroll 8
+              for (int i = l; i < m2o; i += 4) sl = __dadd_rn(sl, __dmul_rn((double)v[i], hp[i * NC]));
+            } else if (l < 2) {
+#pragma unroll 8
+              for (int i = l; i < m2o; i += 2) sl = __dadd_rn(sl, __dmul_rn((double)v[i], hp[i * NC]));
             }
-            __syncthreads();
-            const int nchain = __builtin_popcount(mask) * O;
-            if (t < nchain) {
-              const int o = t % O, c = nth_set_bit(mask, t / O);
-              // position of this column's network in the frame's network list
-              const int pos = c < NG ? 0 : (rbits ? 1 : 0) + __builtin_popcount((mask >> NG) & ((1u << (c - NG)) - 1));
-              if (pos >= g0 && pos < g0 + gn) {
-                const WT *v = w3s + (pos - g0) * per_net + o * C3;
-                const double *hp = h2 + c;
-                const double zz = blas_dot([&](int j) { return (double)v[j]; }, [&](int j) { return hp[j * NC]; },
-                                           C3, blas_kind(o, O));
-                outv[c * 4 + o] = sigmoid_f64_call(zz);
-              }
+            const double s1 = __shfl_xor(sl, 1, 4), s2 = __shfl_xor(sl, 2, 4), s3 = __shfl_xor(sl, 3, 4);
+            if (l == 0) {
+              const double blk = kd == 1 ? __dadd_rn(sl, s1) : __dadd_rn(__dadd_rn(sl, s2), __dadd_rn(s1, s3));
+              const double y = m2o ? __dadd_rn(0.0, blk) : 0.0;
+              const double zz =
+                  blas_tail([&](int i) { return (double)v[i]; }, [&](int i) { return hp[i * NC]; }, m2o, m3o, y);
+              outv[c * 4 + o] = sigmoid_f64_call(zz);
             }
+          };
+          if (w3r) {
+            if (qi < nq) chain(w3r + (c < NG ? 0 : 1 + c - NG) * O * C3 + o * C3);
             __syncthreads();
+          } else {
+            WT *w3s = (WT *)h1;
+            const int per_net = O * C3;
+            const int cap = (C2 * NC * 8) / (per_net * (int)sizeof(WT));
+            const unsigned rbits = mask & ((1u << NG) - 1);
+            // position of this thread's column's network in the frame's network list
+            const int pos = c < NG ? 0 : (rbits ? 1 : 0) + __builtin_popcount((mask >> NG) & ((1u << (c - NG)) - 1));
+            for (int g0 = 0; g0 < n_nets; g0 += cap) {
+              const int gn = min(cap, n_nets - g0);
+              // kW3Batch loads in flight per thread before any LDS store (a
+              // load-then-store loop waits out one HBM round trip per element)
+              constexpr int kW3Batch = 8;
+              for (int i0 = t; i0 < gn * per_net; i0 += kW3Batch * kWideThreads) {
+                WT val[kW3Batch];
+#pragma unroll
+                for (int q = 0; q < kW3Batch; ++q) {
+                  const int i = i0 + q * kWideThreads;
+                  const int ii = i < gn * per_net ? i : i0;
+                  const int slot = ii / per_net, net = cf[3 + g0 + slot];
+                  const WT *v = (net == 0 ? gbase : opponents + orow[net - 1]) + W1n + W2n;
+                  val[q] = v[ii - slot * per_net];
+                }
+#pragma unroll
+                for (int q = 0; q < kW3Batch; ++q)
+                  if (i0 + q * kWideThreads < gn * per_net) w3s[i0 + q * kWideThreads] = val[q];
+              }
+              __syncthreads();
+              if (qi < nq && pos >= g0 && pos < g0 + gn) chain(w3s + (pos - g0) * per_net + o * C3);
+              __syncthreads();
+            }
           }
         }
         PG_STAMP(3);
@@ -504,11 +668,11 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
         if (vis) {
           const int ir = argmax_np(outv + lane * 4, O);
           right = index_to_code(ir);
-          if (p.hard_log && near_tie(outv + lane * 4, O)) log_wide(p, grow, 0, ir, feat + lane * 8);
+          if (p.hard_log && near_tie(outv + lane * 4, O)) log_wide(p.hard_log, p.counters, p.hard_cap, grow, 0, ir, feat + lane * 8);
           if (kind == kOppNN) {
             const int il = argmax_np(outv + (NG + lane) * 4, O);
             left = index_to_code(il);
-            if (p.hard_log && near_tie(outv + (NG + lane) * 4, O)) log_wide(p, p.opp[w], 1, il, feat + (NG + lane) * 8);
+            if (p.hard_log && near_tie(outv + (NG + lane) * 4, O)) log_wide(p.hard_log, p.counters, p.hard_cap, p.opp[w], 1, il, feat + (NG + lane) * 8);
           }
           c_fwd += 1 + (kind == kOppNN ? 1 : 0);
         }
@@ -562,7 +726,8 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   }
 #ifdef PG_WIDE_STAMPS
   if (p.counters && t == 0)
-    for (int i = 0; i < 3; ++i) atomicAdd((unsigned long long *)&p.counters[4 + i], (unsigned long long)stamp_acc[i]);
+    for (int i = 0; i < 5; ++i)
+      atomicAdd((unsigned long long *)&p.counters[i < 3 ? 4 + i : 7 + i], (unsigned long long)stamp_acc[i]);
 #endif
   if (p.counters && t == 0 && c_streams)  // network passes: each streams W1, W2, W3 of one network once
     atomicAdd((unsigned long long *)&p.counters[7], (unsigned long long)c_streams);
@@ -574,25 +739,44 @@ bool wide_shape_ok(const pg_net &n, int n_games) {
          n_games >= 1 && n_games <= kWideMaxGames;
 }
 
+static int wide_groups(int n_games) { return n_games <= 6 ? 6 : 8; }
+
+static int wide_grid(int n_genomes) {
+  const int cap = num_cus();
+  return n_genomes < cap ? n_genomes : cap;
+}
+
+size_t wide_workspace_bytes(const pg_eval_args *a) {
+  if (!a || a->n_genomes <= 0 || a->net.n_nodes != 4) return 0;
+  const int NG = wide_groups(a->n_games);
+  const WideLayout l = wide_layout(a->net.nodes[1], a->net.nodes[2], a->net.bias ? 1 : 0,
+                                   a->net.dtype == PG_F64 ? 8 : 4);
+  return (size_t)wide_grid(a->n_genomes) * (size_t)(NG + 1) * (size_t)l.net_bytes;
+}
+
 template <int NG, typename WT>
-static int32_t launch_wide_t(const EvalParams &p, hipStream_t s) {
-  const int lds = wide_lds_bytes(2 * NG, p.nodes[1], p.nodes[2], p.bias);
+static int32_t launch_wide_t(EvalParams p, void *scratch, hipStream_t s) {
+  int lds = wide_lds_bytes(2 * NG, p.nodes[1], p.nodes[2], p.bias);
   if (lds > 160 * 1024) return fail(PG_ERR_UNSUPPORTED, "k_wide needs %d bytes of LDS", lds);
+  // W3 resident for the genome's games when it fits beside h1 / h2 (config 5 in f32: 43 KB)
+  const int w3_bytes = align16((NG + 1) * p.nodes[3] * (p.nodes[2] + p.bias) * (int)sizeof(WT));
+  p.wide_w3_resident = lds + w3_bytes <= 160 * 1024 ? 1 : 0;
+  if (p.wide_w3_resident) lds += w3_bytes;
   // above 64 KB of dynamic LDS; an older runtime that rejects the attribute launches anyway
   (void)hipFuncSetAttribute((const void *)k_wide<NG, WT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   (void)hipGetLastError();
-  const int cap = num_cus();
-  const int grid = p.n_genomes < cap ? p.n_genomes : cap;
+  const int grid = wide_grid(p.n_genomes);  // wide_workspace_bytes sized the scratch for this grid
   if (grid <= 0) return PG_OK;
+  p.wide_scratch = scratch;
   hipLaunchKernelGGL((k_wide<NG, WT>), dim3(grid), dim3(kWideThreads), (size_t)lds, s, p);
   PG_HIP(hipGetLastError());
   return PG_OK;
 }
 
-int32_t launch_wide(const EvalParams &p, int dtype, hipStream_t s) {
-  if (p.n_games <= 6)
-    return dtype == PG_F64 ? launch_wide_t<6, double>(p, s) : launch_wide_t<6, float>(p, s);
-  return dtype == PG_F64 ? launch_wide_t<8, double>(p, s) : launch_wide_t<8, float>(p, s);
+int32_t launch_wide(const EvalParams &p, int dtype, void *scratch, hipStream_t s) {
+  if (wide_groups(p.n_games) == 6)
+    return dtype == PG_F64 ? launch_wide_t<6, double>(p, scratch, s) : launch_wide_t<6, float>(p, scratch, s);
+  return dtype == PG_F64 ? launch_wide_t<8, double>(p, scratch, s) : launch_wide_t<8, float>(p, scratch, s);
 }
 
 }  // namespace pg

@@ -881,9 +881,20 @@ static size_t eval_base_workspace(const pg_eval_args *a) {
   return 256 + ((games * sizeof(int32_t) + 255) / 256) * 256;
 }
 
+// the kernel pg_eval_population runs for a (PG_KERNEL_AUTO resolved)
+static int resolve_kernel(const pg_eval_args *a) {
+  if (a->kernel != PG_KERNEL_AUTO) return a->kernel;
+  if (resident_shape_ok(a->net) && a->precision == PG_PREC_CERTIFIED) return PG_KERNEL_SPLIT;
+  if (wide_shape_ok(a->net, a->n_games) && (a->net.nodes[1] >= 64 || a->net.nodes[2] >= 64)) return PG_KERNEL_WIDE;
+  return PG_KERNEL_GENERAL;
+}
+
 size_t pg_eval_workspace_bytes(const pg_eval_args *a) {
   size_t n = eval_base_workspace(a);
-  if (a && a->kernel == PG_KERNEL_STAGED) n += (staged_workspace_bytes(a) + 255) / 256 * 256;
+  if (!a) return n;
+  const int kernel = resolve_kernel(a);
+  if (kernel == PG_KERNEL_STAGED) n += (staged_workspace_bytes(a) + 255) / 256 * 256;
+  if (kernel == PG_KERNEL_WIDE && wide_shape_ok(a->net, a->n_games)) n += (wide_workspace_bytes(a) + 255) / 256 * 256;
   return n;
 }
 
@@ -954,21 +965,13 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   p.max_width = max_width(a->net);
 
   PG_HIP(hipMemsetAsync(a->workspace, 0, 256, s));
-  int kernel = a->kernel;
+  const int kernel = resolve_kernel(a);
   const bool res_ok = resident_shape_ok(a->net);
   const bool wide_ok = wide_shape_ok(a->net, a->n_games);
-  if (kernel == PG_KERNEL_AUTO) {
-    if (res_ok && a->precision == PG_PREC_CERTIFIED)
-      kernel = PG_KERNEL_SPLIT;
-    else if (wide_ok && (a->net.nodes[1] >= 64 || a->net.nodes[2] >= 64))
-      kernel = PG_KERNEL_WIDE;
-    else
-      kernel = PG_KERNEL_GENERAL;
-  }
   if (kernel == PG_KERNEL_WIDE) {
     if (!wide_ok)
       return fail(PG_ERR_UNSUPPORTED, "wide kernel needs NETWORK_SHAPE [6, H1<=512, H2<=512, 1..4] and n_games <= 8");
-    rc = launch_wide(p, a->net.dtype, s);
+    rc = launch_wide(p, a->net.dtype, (char *)a->workspace + eval_base_workspace(a), s);
     if (rc != PG_OK) return rc;
   } else if (kernel == PG_KERNEL_SPLIT) {
     if (!res_ok) return fail(PG_ERR_UNSUPPORTED, "split kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");

@@ -42,13 +42,16 @@ def one(args):
         ms.append(a.elapsed_time(b))
         c = res.counters.cpu()
         steps, fwd, slow, fails, plateau, tight = int(c[0]), int(c[1]), int(c[2]), int(c[4]), int(c[5]), int(c[6])
+        passes = int(c[7])  # k_wide: network weight passes (each streams one network's genes once)
+        c10, c11 = int(c[10]), int(c[11])  # k_wide stamps build: D and prep cycles
     mean = sum(ms) / len(ms)
     print(json.dumps({"lib": os.path.basename(os.environ.get("PONG_GA_LIB", "default")), "lanes": args.lane,
                       "kernel": args.kernel,
                       "shape": shape, "kernel_ms": mean, "min_ms": min(ms), "env_steps": steps,
                       "env_steps_per_s": steps / (mean / 1e3), "fwd": fwd, "f64_redecide": slow,
                       "cert_fail": fails, "inwave_plateau": tight, "service_certified": plateau,
-                      "memo_hits": fails - tight - plateau - slow}), flush=True)
+                      "memo_hits": fails - tight - plateau - slow, "passes": passes, "c10": c10, "c11": c11,
+                      "stream_TBps": passes * ev.genes * ev.dtype.itemsize / (mean / 1e3) / 1e12}), flush=True)
 
 
 def main():
