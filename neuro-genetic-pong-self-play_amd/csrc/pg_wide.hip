@@ -48,6 +48,15 @@ constexpr bool kBurst = false;
 #else
 constexpr bool kBurst = true;
 #endif
+// Cache policy of the W2 stream's loads: non-temporal (the cache-policy
+// operand's nt bit), so the stream does not evict what the frame re-reads
+// (W1 rows, h tables, the sigmoid table) -- 930 -> 851 ms per launch at pop
+// 4096 (profiles/r02/sweep_wide_c8.log); -DPG_WIDE_PLAIN: default policy.
+#ifdef PG_WIDE_PLAIN
+constexpr int kStreamPolicy = 0;
+#else
+constexpr int kStreamPolicy = 2;
+#endif
 // A scheduling fence after each 16-B piece of a tile: the scheduler would
 // otherwise hoist the LDS reads of all 32 columns' activations to the top of
 // the tile and spill the partial sums.
@@ -352,13 +361,13 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           return r;
         };
         auto load = [&](const Src &src, int q) -> uint4 {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, t * 16, src.soff + q * PB, 0);
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, t * 16, src.soff + q * PB, kStreamPolicy);
           return make_uint4(v[0], v[1], v[2], v[3]);
         };
         auto load_tail = [&](const Src &src, uint4 (&rt)[kTP]) {
 #pragma unroll
           for (int i = 0; i < kTP; ++i) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, src.toff + i * PB, 0, 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, src.toff + i * PB, 0, kStreamPolicy);
             rt[i] = make_uint4(v[0], v[1], v[2], v[3]);
           }
         };
@@ -375,6 +384,22 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             }
           }
         };
+        const int j = t;
+        WT w1[NG + 1][7];
+        auto load_w1 = [&]() {
+          if (j < H1) {
+#pragma unroll
+            for (int n = 0; n <= NG; ++n) {
+              const bool need = n == 0 ? (mask & ((1u << NG) - 1)) != 0 : ((mask >> (NG + n - 1)) & 1) != 0;
+              const WT *row = (n == 0 ? gbase : opponents + orow[n == 0 ? 0 : n - 1]) + (long)j * C1;
+#pragma unroll
+              for (int i = 0; i < 7; ++i) w1[n][i] = (need && i < C1) ? row[i] : WT(0);
+            }
+          }
+        };
+#ifdef PG_WIDE_W1_FIRST  // experiment: W1 requested ahead of the tiles
+        load_w1();
+#endif
 #ifndef PG_WIDE_LATE_PROLOGUE
         prologue();
 #endif
@@ -386,17 +411,9 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
         // go to h1, then the inlined sigmoid runs over all columns, four at a
         // time (unneeded columns compute garbage nobody reads; no call: the
         // tiles in flight stay in VGPRs).
-        const int j = t;
-        WT w1[NG + 1][7];
-        if (j < H1) {
-#pragma unroll
-          for (int n = 0; n <= NG; ++n) {
-            const bool need = n == 0 ? (mask & ((1u << NG) - 1)) != 0 : ((mask >> (NG + n - 1)) & 1) != 0;
-            const WT *row = (n == 0 ? gbase : opponents + orow[n == 0 ? 0 : n - 1]) + (long)j * C1;
-#pragma unroll
-            for (int i = 0; i < 7; ++i) w1[n][i] = (need && i < C1) ? row[i] : WT(0);
-          }
-        }
+#ifndef PG_WIDE_W1_FIRST
+        load_w1();
+#endif
         if (j < H1) {
 #pragma unroll
           for (int c = 0; c < NC; ++c) {

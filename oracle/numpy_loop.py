@@ -242,6 +242,18 @@ def evaluate(nodes, genes, kinds, opp_rows, mults, opponents, base_seed=0):
 
 
 def _worker(job):
+    """One BLAS thread per worker: the pool is the parallelism (as SCOOP's
+    worker processes are); an OpenBLAS pool per process would oversubscribe
+    the cores (16 processes x OMP_NUM_THREADS threads on the GPU box)."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:  # timing helper: run as is without it
+        return _games(job)
+    with threadpool_limits(1):
+        return _games(job)
+
+
+def _games(job):
     nodes, genomes, kinds, opps, mults, opponents, deadline, seed = job
     np.random.seed(seed)
     steps, games = 0, 0
