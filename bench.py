@@ -84,14 +84,17 @@ def main():
     # path on a one-GPU box (ranks share devices); the driver's runs use RCCL
     backend = os.environ.get("PG_DIST_BACKEND", "nccl")
     local_dev = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
-    if world > 1:
+    # PG_FORCE_DIST=1 runs the N > 1 path (process group, barriers, max-over-ranks
+    # timing, the fitness all-gather) at any world size, e.g. RCCL at N = 1
+    dist_on = world > 1 or os.environ.get("PG_FORCE_DIST") == "1"
+    if dist_on:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local_dev)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
         else:
             dist.init_process_group(backend)
-    dev = torch.device("cuda", local_dev if world > 1 else 0)
+    dev = torch.device("cuda", local_dev if dist_on else 0)
     torch.cuda.set_device(dev)
 
     from pong_amd import build as B
@@ -136,7 +139,7 @@ def main():
     for w in range(args.warmup):
         ga.step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -157,7 +160,7 @@ def main():
         kernel_ms.append(ev_start.elapsed_time(ev_end))
     ga.eval_events = None
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -174,7 +177,7 @@ def main():
     t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)]
                      + [float(v) for v in cert_local] + [float(passes_local), float(skip_local)],
                      dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         tsum = t.clone()
@@ -227,6 +230,7 @@ def main():
                        "population": P, "population_per_gpu": n_local, "network_shape": shape,
                        "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                        "parallelism": f"dp{world}" if world > 1 else "dp1",
+                   "process_group": (dist.get_backend() if dist.is_initialized() else None),
                        "env_steps_per_generation": steps_all / args.steps,
                        "periodic_rally_frames_skipped_per_generation": skip_all / args.steps,
                        "episode_frames_per_sec_incl_skipped": (steps_all + skip_all) / elapsed,
@@ -241,7 +245,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args, shape, ga, pool=cpu_pool)
             cpu_pool.close()
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 
@@ -313,6 +317,7 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
                    "population": P, "population_per_gpu": n_local, "network_shape": shape,
                    "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                    "parallelism": f"dp{world}" if world > 1 else "dp1",
+                   "process_group": (dist.get_backend() if dist.is_initialized() else None),
                    "env_steps_per_generation": steps_all / args.steps,
                    "periodic_rally_frames_skipped_per_generation": skip_all / args.steps,
                    "network_passes_per_generation": passes_all / args.steps,

@@ -205,7 +205,9 @@ class DeviceGA:
             shard = torch.zeros(n, dtype=torch.float64, device=self.device)
             shard[local.long() - lo] = fit
             fit = torch.where(inv_s, shard, torch.zeros_like(shard))
-        return PD.gather_fitness(fit, self.P, self.group) if self.world > 1 else fit
+        # with a process group the all-gather runs at any world size (at N = 1 a
+        # one-rank RCCL collective: the N > 1 code path, exercised on one GPU)
+        return PD.gather_fitness(fit, self.P, self.group) if dist.is_initialized() else fit
 
     @staticmethod
     def _check(fit: torch.Tensor):
