@@ -3,7 +3,7 @@
 
 Needs a library built with -DPG_TIMELINE (PONG_GA_LIB=...): the split kernel
 then writes {start, end, block, thread} (s_memrealtime, 100 MHz) per game into
-the trace buffer instead of actions.  Prints how the launch drains: games
+the trace buffer instead of actions (and the block and wave that ran it).  Prints how the launch drains: games
 still running over time, and when the longest games started.
 usage: PONG_GA_LIB=variants/timeline.so python tools/timeline.py [--pop 65536] [--lanes 8]
 """
@@ -37,9 +37,9 @@ def main():
     total = n * ev.n_games
     ev.evaluate(genomes, kind, opp, mult, opponents=hof)  # warm-up
     torch.cuda.synchronize()
-    res, tr = ev.evaluate(genomes, kind, opp, mult, opponents=hof, trace_games=total, trace_cap=16)
+    res, tr = ev.evaluate(genomes, kind, opp, mult, opponents=hof, trace_games=total, trace_cap=24)
     torch.cuda.synchronize()
-    tl = tr.cpu().numpy().view(np.uint32).reshape(total, 4).astype(np.int64)
+    tl = tr.cpu().numpy().view(np.uint32).reshape(total, 6).astype(np.int64)
     frames = res.frames.cpu().numpy().reshape(-1)
     t0 = tl[:, 0].min()
     start = (tl[:, 0] - t0) / 100.0  # us
@@ -66,6 +66,13 @@ def main():
         coef, *_ = np.linalg.lstsq(A, dur[m] / frames[m], rcond=None)
         out["fit_us_per_frame"] = float(coef[0])
         out["fit_us_per_trip"] = float(coef[1])
+    # per game-wave index: frames per microsecond of wall time summed over each
+    # wave's games (wave w runs on SIMD w % 4; the service wave shares SIMD 3)
+    wave = tl[:, 5]
+    out["frames_per_us_by_wave"] = {int(v): float(frames[wave == v].sum() / dur[wave == v].sum())
+                                    for v in np.unique(wave)}
+    out["us_per_frame_median_by_wave"] = {int(v): float(np.median(dur[wave == v] / np.maximum(frames[wave == v], 1)))
+                                          for v in np.unique(wave)}
     grid = np.linspace(0, span, 21)
     out["running_games"] = [int(((start <= t) & (end > t)).sum()) for t in grid]
     print(json.dumps(out), flush=True)
