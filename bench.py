@@ -121,6 +121,7 @@ def main():
     ga = DeviceGA(shape, P, H, tournsize, dtype=dtype, device=dev, n_games=args.games, schedule="selfplay",
                   seed=args.seed, kernel=args.kernel)
     ga.ev.group_lanes = args.group_lanes
+    ga.order_by_length = os.environ.get("PG_NO_LENGTH_ORDER") != "1"  # A/B switch for the evaluation order
     G = ga.G
     ga.initialize("normal", args.sigma)
     # the first games already face a full hall of fame: H independent random

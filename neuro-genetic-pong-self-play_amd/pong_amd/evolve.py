@@ -88,6 +88,13 @@ class DeviceGA:
         self._next = None        # (generation, inv, inherited): offspring already varied into spare[H:]
         self.hard_log = None     # optional [cap, 8] int32: the evaluation's hard decisions (pg_eval_args.hard_log)
         self.on_evaluate = None  # optional callable(g, rows, opponents, result), right after each evaluation
+        # Evaluation order: a genome's longest game sets when its last game ends,
+        # and a long game started late sets the launch's tail.  Each row carries
+        # the longest game of its lineage's last evaluation (a child inherits its
+        # parent's); the shard's invalid rows are played longest-first.  Order
+        # only: every game's result is the same in any order.
+        self.order_by_length = True
+        self.lineage_frames = torch.zeros(self.P, dtype=torch.float32, device=self.device)
 
     # ------------------------------------------------------------ views
     @property
@@ -179,10 +186,15 @@ class DeviceGA:
             inv_s = inv[lo:hi]
             c_inv = torch.cumsum(inv_s, 0, dtype=torch.int32)
             count = c_inv[-1:] if n else torch.zeros(1, dtype=torch.int32, device=self.device)
-            c_val = torch.cumsum(~inv_s, 0, dtype=torch.int32)
-            dest = torch.where(inv_s, c_inv - 1, count + c_val - 1).long()
-            local = torch.empty(n, dtype=torch.int32, device=self.device)
-            local[dest] = torch.arange(lo, hi, dtype=torch.int32, device=self.device)  # invalid rows first
+            if self.order_by_length:
+                # invalid rows first, longest predicted game first (clones key -1, last)
+                key = torch.where(inv_s, self.lineage_frames[lo:hi], torch.full_like(self.lineage_frames[lo:hi], -1.0))
+                local = (torch.argsort(key, descending=True, stable=True) + lo).to(torch.int32)
+            else:
+                c_val = torch.cumsum(~inv_s, 0, dtype=torch.int32)
+                dest = torch.where(inv_s, c_inv - 1, count + c_val - 1).long()
+                local = torch.empty(n, dtype=torch.int32, device=self.device)
+                local[dest] = torch.arange(lo, hi, dtype=torch.int32, device=self.device)  # invalid rows first
         kind, opp, mult = D.schedule(self.schedule, n, self.n_games, lo, self.hof_fitness, self.hof_n,
                                      self.seed, g, self.device, rows=local)
         opponents = self.store[: self.hof_n] if self.hof_n else None
@@ -200,6 +212,13 @@ class DeviceGA:
         self.last, self.last_rows, self.last_count = res, local, count
         if self.on_evaluate is not None:
             self.on_evaluate(g, rows if local is not None else rows[lo:hi], opponents, res)
+        longest = res.frames.max(dim=1).values.to(torch.float32)
+        if local is None:
+            self.lineage_frames[lo:hi] = longest
+        else:  # the played rows' longest games; clones keep their lineage's
+            played = torch.arange(n, device=self.device) < count
+            at = local.long()
+            self.lineage_frames[at] = torch.where(played, longest, self.lineage_frames[at])
         fit = res.fitness
         if local is not None:  # back to shard order; rows not played (clones) read 0
             shard = torch.zeros(n, dtype=torch.float64, device=self.device)
@@ -221,6 +240,7 @@ class DeviceGA:
         _, invalid = D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu,
                             self.sigma, self.indpb, seed=self.seed, generation=g, out=out)
         inherited = fitness[chosen.long()]  # a clone keeps its parent's fitness (varAnd)
+        self.lineage_frames = self.lineage_frames[chosen.long()]  # and its parent's game lengths
         return invalid.bool(), inherited
 
     def _hof_update(self, fit: torch.Tensor, rows: torch.Tensor, dst: torch.Tensor, overlap=None):
