@@ -506,7 +506,6 @@ struct SlowSlot {
   int n_memo;  // decisions memoised for the current game's network (the owning group only)
   uint64_t memo_key[kMemo];
   int memo_idx[kMemo];
-  uint64_t pend_key;   // k_inwave: the memo key of the pending request
   uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
   int rally_at, rally_span;
 };

@@ -302,299 +302,16 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   if (lane64 == 0) atomicAdd(&waves_done, 1);
 }
 
-// ============================================================ k_inwave ====
-// k_service's game loop with no service wave: every wave of the block plays
-// games, and a wave whose half-groups need the f64 cascade runs it itself,
-// with all 64 lanes, at a point of the frame where the wave has reconverged.
-// Why: the hardware favours the older waves of a SIMD (waves 0-3 ran frames at
-// 0.88 per us, 4-6 at 0.67, tools/timeline.py), so the service wave's SIMD
-// carried one game wave instead of two (profiles/r02/timeline_by_wave.log).
-// Each frame is split in two halves around that point: (1) game start,
-// physics, features, f32 forward, certificate, in-wave plateau rule, memo
-// lookup, and -- on a miss -- the request written to the half-group's LDS
-// slot; (2) the answer, the memo update, decisions, clamps, bookkeeping,
-// termination.  Groups that ran out of games stay in the loop, idle, until
-// the whole wave has.
-#ifndef PG_INWAVE_SERVE_ATTR
-#define PG_INWAVE_SERVE_ATTR __forceinline__
-#endif
-// k_inwave's f64 cascade for the request in one slot, by a whole wave (all 64
-// lanes active).  Out of line: the game loop's registers are saved only
-// around this (rare) call, not spilled throughout the frame (inlined, the
-// cascade's register needs made the allocator spill inside the hot frame:
-// 70 vs 11 ms per launch).  Fields by value, not the EvalParams: a reference
-// would copy the kernel's parameter block to private memory.
-template <int HL, int U, int O, typename WT>
-__device__ PG_INWAVE_SERVE_ATTR int inwave_serve(const SlowSlot *slot, int H, int b, double *lds_f64, int lane64,
-                                         uint32_t *hard_log, uint64_t *counters, int hard_cap, const WT *genomes,
-                                         const WT *opponents, int n_opponents, int64_t gstride, int64_t ostride) {
-  const WT *g = (const WT *)slot->g;
-  int k[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) k[i] = slot->k[i];
-  float zf[O];
-#pragma unroll
-  for (int o = 0; o < O; ++o) zf[o] = slot->z[o];
-  int ans = plateau_decide<O>(zf, slot->e, lane64);
-  if (ans < 0) ans = fast_f64_decide<O, WT>(g, H, b, k, lane64);
-  if (ans < 0) {
-    ans = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_f64, lane64);
-    if (hard_log && lane64 == 0) {
-      const long oo = g - opponents;
-      const bool opp = opponents != genomes && oo >= 0 && oo < (long)n_opponents * ostride;
-      log_hard_raw(hard_log, counters, hard_cap, (int)(opp ? oo / ostride : (g - genomes) / gstride), opp ? 1 : 0,
-                   ans, 0, k);
-    }
-    return ans | 256;
-  }
-  return ans | 512;
-}
-
-template <int L, int U, int O, typename WT>
-__global__ __launch_bounds__(svc_threads<U>()) void k_inwave(EvalParams p) {
-  constexpr int kThreads = svc_threads<U>();
-  constexpr int HL = L / 2;
-  constexpr int kSlots = (kThreads / L) * 2;
-  __shared__ SlowSlot slots[kSlots];
-  extern __shared__ double lds_svc[];  // [waves][f64_lds_doubles(H, O)]
-  const int H = p.nodes[1];
-  const int b = p.bias;
-  const int wave = threadIdx.x >> 6;
-  const int lane64 = threadIdx.x & 63;
-  double *lds_f64 = lds_svc + wave * f64_lds_doubles(H, O);
-
-  const int lig = threadIdx.x & (L - 1);
-  const int side = lig >= HL ? 1 : 0;  // 0: right paddle's network, 1: left paddle's
-  const int hl = lig & (HL - 1);
-  const int leader = lane64 & ~(L - 1);
-  const int sx = (threadIdx.x / L) * 2 + side;
-  const WT *genomes = (const WT *)p.genomes;
-  const WT *opponents = (const WT *)p.opponents;
-
-  NetP<U, O> net;
-  Pong st;
-  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
-  const WT *gm = genomes;
-  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0;
-
-  const int games_total = active_total(p);
-  int w;
-  {
-    int ww = 0;
-    if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
-    w = group_broadcast<L>(ww, leader);
-  }
-  bool fresh = true;
-  for (;;) {
-    const bool act = w < games_total;
-    if (__ballot(act) == 0) break;
-    // (1) ------------------------------------------------------------------
-    // what (2) needs, packed into one register (bit 0 vis, 1 pending, 2 score
-    // unchanged, 8.. the decision index); the rest is recomputed from st or
-    // kept in the half-group's LDS slot, so the frame's live set across the
-    // reconvergence point stays that of k_service
-    int fl = 0;
-    if (act) {
-      if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
-        const int i = w / p.n_games;
-        const int g = w - i * p.n_games;
-        kind = p.kind[w];
-        const WT *gr = genomes + (long)genome_row(p, i) * p.gstride;
-        gm = (side && kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
-        load_net_pk<HL, U, O, WT>(net, gm, H, b, hl, side);  // the left network with the x-flip folded in
-        st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
-        act_r = act_l = timeout = total = frames = 0;
-        fresh = false;
-        if (hl == 0) slots[sx].n_memo = 0;
-      }
-      const int s1b = st.s1, s2b = st.s2;
-      const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
-      st.step(act_r, act_l);
-      frames += 1;
-      const int vis = st.vis;
-      fl = vis | ((st.s1 == s1b && st.s2 == s2b) ? 4 : 0);
-      if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
-        const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
-        const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
-        const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
-        const int k[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
-        float acc[O], z[O];
-        partial_pk<U, O>(net, k, acc);
-#pragma unroll
-        for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
-        int idx = certify<O>(z, net.e);
-        if (side && kind != kOppNN) idx = 0;  // the left half is idle against a scripted opponent
-        if (idx < 0) {  // rare, half-uniform: the in-wave plateau rule, the memo, else the f64 cascade
-          fails += 1;
-          idx = plateau_f32<O>(z, net.e);
-          inwave += idx >= 0 ? 1 : 0;
-        }
-        if (idx < 0) {
-          const uint64_t key = memo_key(k);
-          const int nm = slots[sx].n_memo;
-          int hit = -1;
-#pragma unroll 1
-          for (int c = 0; c < kMemo && c < nm; ++c)
-            if (slots[sx].memo_key[c] == key) hit = slots[sx].memo_idx[c];
-          if (hit != -1) {
-            idx = hit;
-          } else {
-            idx = 0;
-            fl |= 2;
-            if (hl == 0) {
-              // the network's own features (x-flipped for the left paddle): the f64 path uses the genes
-              const int kn[6] = {side ? 320 - bx2 : bx2, by2, side ? 320 - lbx2 : lbx2, lby2, side ? lc2 : rc2,
-                                 side ? rc2 : lc2};
-              slots[sx].g = gm;
-#pragma unroll
-              for (int i = 0; i < 6; ++i) slots[sx].k[i] = kn[i];
-#pragma unroll
-              for (int o = 0; o < O; ++o) slots[sx].z[o] = z[o];
-              slots[sx].e = net.e;
-              slots[sx].pend_key = key;
-            }
-          }
-        }
-        fl |= idx << 8;
-      }
-    }
-    // -- the wave has reconverged: its f64 re-decisions, one request at a time,
-    // by all 64 lanes (bit 8 / bit 9 of the answer: decided by the numpy-order
-    // forward / by the certified one)
-    uint64_t need = __ballot((fl & 2) && hl == 0);
-    // cold: the register allocator weighs spill placement by block frequency,
-    // and an unhinted loop here counts as hot
-    if (__builtin_expect(need != 0, 0)) {
-    wave_lds_sync();  // the requests written by other lanes of this wave
-    do {
-      const int src = __builtin_ctzll(need);
-      need &= need - 1;
-      const int sl = ((wave * 64 + src) / L) * 2 + ((src & (L - 1)) >= HL ? 1 : 0);  // that half-group's sx
-      const int ans = inwave_serve<HL, U, O, WT>(&slots[sl], H, b, lds_f64, lane64, p.hard_log, p.counters, p.hard_cap,
-                                                 genomes, opponents, p.n_opponents, p.gstride, p.ostride);
-      if (lane64 == 0) slots[sl].idx = ans;
-      wave_lds_sync();  // the answer, for the requesting half-group's lanes
-    } while (need);
-    }
-    // (2) ------------------------------------------------------------------
-    if (act) {
-      int left = 0, right = 0;
-      const int vis = fl & 1;
-      const int by2 = 2 * st.by + kBallH - 1;
-      const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
-      if (vis) {
-        int idx = fl >> 8;
-        if (fl & 2) {
-          const int ans = slots[sx].idx;
-          slow += (ans >> 8) & 1;
-          plateau += ans >> 9;
-          idx = ans & 255;
-          if (hl == 0) {
-            const int nm = slots[sx].n_memo;
-            const int c = nm % kMemo;  // round-robin replacement
-            slots[sx].memo_key[c] = slots[sx].pend_key;
-            slots[sx].memo_idx[c] = idx;
-            slots[sx].n_memo = nm + 1;
-          }
-        }
-        const bool left_nn = kind == kOppNN;
-        const int mine = index_to_code(idx);
-        const int other = other_half<L>(mine);
-        right = side ? other : mine;
-        if (left_nn) {
-          left = side ? mine : other;
-        } else {  // HardcodedAi / ScoreHardcodedAi (dumb_ais.py), group-uniform: skipped in self-play
-          left = hardcoded(by2, lc2);
-          if (kind == kOppScore && st.s1 > st.s2) left = 0;
-        }
-        c_fwd += left_nn ? 2 : 1;
-      }
-      act_l = clamp_action(lc2, left);
-      act_r = clamp_action(rc2, right);
-      if (p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
-        if (w < p.trace_games && frames <= p.trace_cap && lig == 0)
-          p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
-      }
-      if (frames > 1) {
-        if (fl & 4) {
-          timeout += 1;
-        } else {
-          total += timeout;
-          timeout = 0;
-        }
-      }
-#ifndef PG_NO_RALLY_SKIP
-      // a periodic rally ends at the timeout with nothing else changed: jump there
-      // (never while tracing, which records every frame's actions)
-      if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
-          p.trace == nullptr) {
-        const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
-        const uint64_t rkey = rally_key(st, act_r, act_l);
-        if (timeout == kRallyStart) {
-          if (lig == 0) {
-            slots[rs].rally_key = rkey;
-            slots[rs].rally_at = timeout;
-            slots[rs].rally_span = kRallyStart;
-          }
-        } else if (slots[rs].rally_key == rkey) {
-          const int rest = kTimeoutThresh + 1 - timeout;
-          frames += rest;
-          skipped += rest;
-          timeout = kTimeoutThresh + 1;
-        } else if (timeout - slots[rs].rally_at == slots[rs].rally_span) {
-          if (lig == 0) {
-            slots[rs].rally_key = rkey;
-            slots[rs].rally_at = timeout;
-            slots[rs].rally_span = 2 * slots[rs].rally_span;
-          }
-        }
-      }
-#endif
-      if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
-        if (lig == 0) finish_game(p, w, st, frames, total);
-        c_steps += frames;
-        c_games += 1;
-        int ww = 0;
-        if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
-        w = group_broadcast<L>(ww, leader);
-        fresh = true;
-      }
-    }
-  }
-  if (p.counters && c_games) {
-    if (lig == 0) {
-      // env steps simulated: the episodes' frames minus those a periodic rally skipped
-      atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)(c_steps - skipped));
-      atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
-      atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
-      if (skipped) atomicAdd((unsigned long long *)&p.counters[8], (unsigned long long)skipped);
-    }
-    if (hl == 0 && slow) atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
-    if (hl == 0 && fails) atomicAdd((unsigned long long *)&p.counters[4], (unsigned long long)fails);
-    if (hl == 0 && plateau) atomicAdd((unsigned long long *)&p.counters[5], (unsigned long long)plateau);
-    if (hl == 0 && inwave) atomicAdd((unsigned long long *)&p.counters[6], (unsigned long long)inwave);
-  }
-}
-
 template <int L, int U, int O, typename WT>
 inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
   constexpr int kSvcThreads = svc_threads<U>();
-#ifdef PG_SPLIT_INWAVE
-  constexpr int GPB = (kSvcThreads / 64) * (64 / L);  // game groups per block: every wave plays
-  const size_t lds = (size_t)(kSvcThreads / 64) * f64_lds_doubles(p.nodes[1], O) * sizeof(double);
-#else
   constexpr int GPB = (kSvcThreads / 64 - 1) * (64 / L);  // game groups per block
   const size_t lds = (size_t)f64_lds_doubles(p.nodes[1], O) * sizeof(double);
-#endif
   const int want = (p.total + GPB - 1) / GPB;
   const int cap = num_cus() * 2;
   const int grid = want < cap ? want : cap;
   if (grid <= 0) return PG_OK;
-#ifdef PG_SPLIT_INWAVE
-  hipLaunchKernelGGL((k_inwave<L, U, O, WT>), dim3(grid), dim3(kSvcThreads), lds, s, p);
-#else
   hipLaunchKernelGGL((k_service<L, U, O, WT>), dim3(grid), dim3(kSvcThreads), lds, s, p);
-#endif
   PG_HIP(hipGetLastError());
   return PG_OK;
 }
