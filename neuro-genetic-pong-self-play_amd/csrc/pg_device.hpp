@@ -78,10 +78,15 @@ struct Pong {
   // play one game, so a branch only costs the waves where some game takes it.
   __device__ void step(int right_code, int left_code) {
     rpy = move(rpy, dy_of(right_code), kPaddleSpeed);
-    // left paddle: the action, or the built-in CPU of the 1-player env (main.py:40)
-    const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
-    const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
-    lpy = move(lpy, one_player ? cpu_dy : dy_of(left_code), one_player ? kCpuSpeed : kPaddleSpeed);
+    // left paddle: the action, or the built-in CPU of the 1-player env
+    // (main.py:40) -- a branch: no game of a self-play schedule takes it
+    if (__builtin_expect(one_player, 0)) {
+      const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
+      const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
+      lpy = move(lpy, cpu_dy, kCpuSpeed);
+    } else {
+      lpy = move(lpy, dy_of(left_code), kPaddleSpeed);
+    }
 
     constexpr int ymax = kFieldH - kBallH;
     constexpr int lface = kLeftPaddleX + kPaddleW, rface = kRightPaddleX;
