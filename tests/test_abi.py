@@ -79,6 +79,36 @@ def test_validation_errors_without_gpu(lib):
     assert lib.pg_physics_step(None, -1, None, None) == _lib.PG_ERR_INVALID
 
 
+def test_workspace_bytes_follow_the_resolved_kernel(lib):
+    """pg_eval_workspace_bytes sizes the kernel the arguments resolve to (host
+    only, no device: the CU count falls back to 256 without a GPU): the split
+    and general kernels need the base (game counter + per-game flags), the
+    wide kernel adds min(n_genomes, CUs) blocks x 7 tile-major W2 copies
+    (config 5 in f32: 1 056 768 B per copy, its tail piece block included),
+    and AUTO resolves like the launch does."""
+    from pong_amd import _lib
+    a = _lib.PgEvalArgs()
+    a.n_games = 6
+    a.n_genomes = 4096
+    a.kernel = _lib.PG_KERNEL_AUTO
+    base = 256 + (4096 * 6 * 4 + 255) // 256 * 256
+    a.net = _lib.make_net([6, 64, 3])
+    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base
+    a.net = _lib.make_net([6, 512, 512, 3])  # f32 (dtype 0) -> k_wide
+    a.net.dtype = _lib.PG_F32
+    cus = 256
+    per_copy = (16 * 8 + 1) * 512 * 16  # 16 tiles x 8 pieces + 1 tail piece block, 512 rows x 16 B
+    assert per_copy == 1056768
+    wide = base + (min(4096, cus) * 7 * per_copy + 255) // 256 * 256
+    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == wide
+    a.kernel = _lib.PG_KERNEL_GENERAL
+    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base
+    a.kernel = _lib.PG_KERNEL_WIDE
+    a.n_genomes = 3  # fewer genomes than CUs: one block each
+    base3 = 256 + (3 * 6 * 4 + 255) // 256 * 256
+    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base3 + (3 * 7 * per_copy + 255) // 256 * 256
+
+
 def test_struct_layout_matches_c(tmp_path):
     """offsetof/sizeof of every ABI struct from gcc vs the ctypes mirror."""
     from pong_amd import _lib
