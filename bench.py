@@ -358,6 +358,13 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
     from pong_amd import device as D
     O.build()
     lo = ga.lo
+    # host copies bounded by bytes (a wide genome is 2.1 MB in f64): at most
+    # 1 GiB of genomes, per pool worker at most 16 MiB of them (and only the
+    # opponent rows its own games use), C-port chunks of at most 64 MiB
+    row_bytes = ga.G * 8
+    max_rows = max(8, min(max_rows, (1 << 30) // row_bytes))
+    per_worker = max(2, min(64, (16 << 20) // row_bytes))
+    chunk = max(1, min(chunk, (64 << 20) // row_bytes))
     genomes = ga.population[lo:lo + max_rows].double().cpu().numpy()
     n = genomes.shape[0]
     kind, opp, mult = D.schedule(ga.schedule, n, ga.n_games, lo, ga.hof_fitness, ga.hof_n, ga.seed,
@@ -371,7 +378,7 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
     secs = args.cpu_baseline_seconds
     workers = args.cpu_threads
     # numpy loop on `workers` processes, then on one core (~secs and ~secs/2 of wall time)
-    np_rows = min(n, 64 * workers)
+    np_rows = min(n, per_worker * workers)
     rate_p, steps_p, games_p, dt_p = NL.timed_rate(shape, genomes[:np_rows], k[:np_rows], o[:np_rows],
                                                    m[:np_rows], opponents, secs, workers, pool)
     rate_1, steps_1, games_1, dt_1 = NL.timed_rate(shape, genomes[:8], k[:8], o[:8], m[:8], opponents,
@@ -386,9 +393,10 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
         done += chunk
     dt = time.perf_counter() - t0
     return {"value": rate_p, "unit": "env-steps/s", "cores": workers, "kind": "port",
-            "sample": f"the reference's per-frame numpy loop (oracle/numpy_loop.py) on {workers} worker processes: "
-                      f"{games_p} whole games of the same workload's first genomes ({steps_p} env-steps in "
-                      f"{dt_p:.1f} s); {workers} = this box's CPU share per GPU",
+            "sample": f"the reference's per-frame numpy loop (oracle/numpy_loop.py) on {workers} worker processes, "
+                      f"one BLAS thread each: {games_p} whole games of the same workload's first genomes "
+                      f"({steps_p} env-steps; each worker timed on its own clock, at most {dt_p:.1f} s; value = "
+                      f"the sum of the workers' rates); {workers} = this box's CPU share per GPU",
             "one_core": {"value": rate_1, "sample": f"{games_1} games, {steps_1} env-steps in {dt_1:.1f} s"},
             "calibration": "numpy_loop runs 1.11x the reference's own rate on the same games, equal rewards "
                            "(profiles/r02/cpu_calibration.json)",

@@ -254,14 +254,20 @@ def _worker(job):
 
 
 def _games(job):
-    nodes, genomes, kinds, opps, mults, opponents, deadline, seed = job
+    """Whole games until ``seconds`` of this worker's own time have passed
+    (its clock starts when it has its job: shipping the job's genomes to a
+    process is not the reference's per-frame work).  Returns (env-steps,
+    games, busy seconds)."""
+    nodes, genomes, kinds, opps, mults, opponents, seconds, seed = job
     np.random.seed(seed)
+    t0 = time.perf_counter()
+    deadline = t0 + seconds
     steps, games = 0, 0
     for i in range(genomes.shape[0]):
         right = NumpyNet(nodes, genomes[i])
         for g in range(len(kinds[i])):
             if time.perf_counter() >= deadline:
-                return steps, games
+                return steps, games, time.perf_counter() - t0
             k = int(kinds[i][g])
             left = (NumpyNet(nodes, opponents[int(opps[i][g])]) if k == 3
                     else ScoreHardcoded() if k == 2 else Hardcoded())
@@ -269,7 +275,7 @@ def _games(job):
                                                      float(mults[i][g]) if k == 3 else 1.0)
             steps += f
             games += 1
-    return steps, games
+    return steps, games, time.perf_counter() - t0
 
 
 def make_pool(workers):
@@ -281,22 +287,26 @@ def make_pool(workers):
 
 def timed_rate(nodes, genomes, kinds, opps, mults, opponents, seconds, workers=1, pool=None):
     """env-steps/s of whole games (evaluate()'s perform_episode calls, in order)
-    over ``seconds`` of wall time, genomes dealt round-robin to ``workers``
-    processes (as SCOOP's futures.map spreads evaluate() over cores, ga.py:83).
-    Returns (rate, env-steps, games, seconds)."""
-    t0 = time.perf_counter()
-    deadline = t0 + seconds
+    over ``seconds`` of each worker's time, genomes dealt round-robin to
+    ``workers`` processes (as SCOOP's futures.map spreads evaluate() over
+    cores, ga.py:83), all running at once: the rate is the sum of the workers'
+    own rates (env-steps / busy seconds).  Returns (rate, env-steps, games,
+    the longest worker's busy seconds)."""
     if workers <= 1:
-        steps, games = _worker((nodes, genomes, kinds, opps, mults, opponents, deadline, 0))
+        steps, games, dt = _worker((nodes, genomes, kinds, opps, mults, opponents, seconds, 0))
+        return (steps / dt if dt > 0 else 0.0), steps, games, dt
+    jobs = []
+    for w in range(workers):  # each worker gets only the opponent rows its games use
+        ow = np.asarray(opps[w::workers])
+        rows = np.unique(ow)
+        jobs.append((nodes, genomes[w::workers], kinds[w::workers], np.searchsorted(rows, ow).astype(np.int32),
+                     mults[w::workers], opponents[rows], seconds, w))
+    if pool is None:
+        with make_pool(workers) as own:
+            res = own.map(_worker, jobs)
     else:
-        jobs = [(nodes, genomes[w::workers], kinds[w::workers], opps[w::workers], mults[w::workers], opponents,
-                 deadline, w) for w in range(workers)]
-        if pool is None:
-            with make_pool(workers) as own:
-                res = own.map(_worker, jobs)
-        else:
-            res = pool.map(_worker, jobs)
-        steps = sum(r[0] for r in res)
-        games = sum(r[1] for r in res)
-    dt = time.perf_counter() - t0
-    return steps / dt, steps, games, dt
+        res = pool.map(_worker, jobs)
+    steps = sum(r[0] for r in res)
+    games = sum(r[1] for r in res)
+    rate = sum(r[0] / r[2] for r in res if r[2] > 0)
+    return rate, steps, games, max(r[2] for r in res)
