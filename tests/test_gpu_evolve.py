@@ -148,3 +148,40 @@ def test_device_ga_checkpoint_resume(gpu, tmp_path):
     assert torch.equal(d.hall_of_fame, c.hall_of_fame) and bool(d.valid.all())
     rec = d.step()  # eaSimple's generation 0 of the resumed run: nothing to evaluate
     assert rec["nevals"] == 0 and torch.equal(d.fitness, c.fitness)
+
+
+def test_longest_lineage_first_order(gpu):
+    """DeviceGA plays a generation's invalid rows longest-lineage-first
+    (order_by_length): the played rows come in non-increasing order of their
+    lineage's longest game, clones after them, and the population, fitness,
+    hall of fame and logbook equal those of the row-order run."""
+    from pong_amd.evolve import DeviceGA
+    kw = dict(hof_size=24, tournsize=12, device=gpu, schedule="selfplay", seed=13)
+    runs, checked = {}, []
+    for order in (True, False):
+        ga = DeviceGA([6, 8, 3], 160, **kw)
+        ga.order_by_length = order
+
+        def probe(g, rows, opponents, res, ga=ga, order=order):
+            # called before the evaluation's results update the predictions:
+            # lineage_frames still holds the key the order was made with
+            if order and ga.last_rows is not None:
+                m = int(ga.last_count[0])
+                key = ga.lineage_frames[ga.last_rows[:m].long()].cpu().numpy()
+                assert (key[:-1] >= key[1:]).all(), key
+                played = set(ga.last_rows[:m].cpu().tolist())
+                assert len(played) == m
+                checked.append(m)
+
+        ga.on_evaluate = probe
+        ga.initialize("normal", 3.0)
+        for _ in range(4):
+            ga.step()
+        runs[order] = ga
+    a, b = runs[True], runs[False]
+    assert len(checked) == 3 and min(checked) > 0
+    assert torch.equal(a.population, b.population) and torch.equal(a.fitness, b.fitness)
+    assert torch.equal(a.hall_of_fame, b.hall_of_fame)
+    assert a.hof_member_fitness.tolist() == b.hof_member_fitness.tolist()
+    assert a.logbook == b.logbook
+    assert bool((a.lineage_frames > 0).any())
