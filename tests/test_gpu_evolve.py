@@ -179,7 +179,7 @@ def test_longest_lineage_first_order(gpu):
             ga.step()
         runs[order] = ga
     a, b = runs[True], runs[False]
-    assert len(checked) == 3 and min(checked) > 0
+    assert len(checked) == 4 and min(checked) > 0  # the initial evaluation and three generations
     assert torch.equal(a.population, b.population) and torch.equal(a.fitness, b.fitness)
     assert torch.equal(a.hall_of_fame, b.hall_of_fame)
     assert a.hof_member_fitness.tolist() == b.hof_member_fitness.tolist()
