@@ -477,10 +477,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
         auto compute = [&](int s, uint4 (&r)[8], uint4 (&rt)[kTP], int sn) {
           const Src src = source(sn);
           // rows t >= H2 of a partial last wave sum garbage that is never stored
-          bool work = s < S;
-#ifdef PG_WIDE_NOCOMPUTE
-          work = false;  // diagnostic build: streaming only
-#endif
+          const bool work = s < S;
           if (!work) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) r[q] = load(src, q);
