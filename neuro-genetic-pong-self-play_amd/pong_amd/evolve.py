@@ -95,20 +95,6 @@ class DeviceGA:
         # only: every game's result is the same in any order.
         self.order_by_length = True
         self.lineage_frames = torch.zeros(self.P, dtype=torch.float32, device=self.device)
-        if self.H and self.device.type == "cuda":
-            self._preload_prepare_kernels()
-
-    def _preload_prepare_kernels(self):
-        """Run the hall-of-fame prepare's sorts once in each of torch's sort
-        regimes (in-place bitonic up to 32 keys, in-place block radix up to
-        4096, device-wide radix above), so their code objects load here and
-        not (~15 ms each, measured) in the generation where the candidate
-        count first drops below 4096."""
-        for k in (8, 1000, 8192):
-            f = torch.zeros(k, dtype=torch.float64, device=self.device)
-            hof_ranks(f[: k // 2], f)
-            dense_classes(torch.zeros(k, dtype=torch.int64, device=self.device))
-        torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------ views
     @property
@@ -257,21 +243,16 @@ class DeviceGA:
         self.lineage_frames = self.lineage_frames[chosen.long()]  # and its parent's game lengths
         return invalid.bool(), inherited
 
-    def _hof_update(self, fit: torch.Tensor, rows: torch.Tensor, dst: torch.Tensor, overlap=None,
-                    summary: Optional[torch.Tensor] = None):
+    def _hof_update(self, fit: torch.Tensor, rows: torch.Tensor, dst: torch.Tensor, overlap=None):
         """HallOfFame.update(rows) with fitness ``fit``; the members are gathered
         into dst[:new_n] (dst is disjoint from the current members and rows).
         ``overlap`` (a callable enqueueing device work that touches none of
         these rows) runs once the host scan's inputs are copied out, so the
-        device executes it while the host scans.  ``summary`` (a small f64
-        device vector) rides along in the scan's one device->host copy and is
-        returned as a list; the host checks it (``_check_summary``) before
-        the scan reads any fitness."""
+        device executes it while the host scans."""
         if self.H == 0:
-            vals = self._check_summary(summary)
             if overlap:
                 overlap()
-            return vals
+            return
         old_n = self.hof_n
         if old_n >= self.H:
             # a full hall only admits fitness > its worst, and the worst only rises:
@@ -281,11 +262,10 @@ class DeviceGA:
             cand = torch.arange(self.P, device=self.device)
         k = int(cand.numel())
         if k == 0:
-            vals = self._check_summary(summary)
             dst[:old_n] = self.store[:old_n]
             if overlap:
                 overlap()
-            return vals
+            return
         h = D.row_hash(rows, self.G, index=cand.to(torch.int32))
         fc = fit[cand]
         # Everything the sequential scan needs, computed on the device and sent
@@ -295,13 +275,14 @@ class DeviceGA:
         n = old_n + k
         if self.profile is not None:
             self.profile["hof_candidates"] = self.profile.get("hof_candidates", 0) + k
-        rank = hof_ranks(self.hof_fitness[:old_n], fc)
+        by_age = torch.cat([self.hof_fitness[:old_n].flip(0), fc])
+        order = torch.sort(by_age, stable=True).indices
+        rank_age = torch.empty_like(order)
+        rank_age[order] = torch.arange(n, device=self.device)
+        rank = torch.cat([rank_age[:old_n].flip(0), rank_age[old_n:]])
         hashes = torch.cat([self.hof_hash[:old_n], h])
-        cls = dense_classes(hashes)
-        parts = [rank | (cls << 32), fc.view(torch.int64)]
-        if summary is not None:
-            parts.append(summary.view(torch.int64))
-        packed_d = torch.cat(parts)
+        cls = torch.unique(hashes, return_inverse=True)[1]
+        packed_d = torch.cat([rank | (cls << 32), fc.view(torch.int64)])
         packed_h = torch.empty(packed_d.shape, dtype=torch.int64, pin_memory=True)
         packed_h.copy_(packed_d, non_blocking=True)
         copied = torch.cuda.Event()
@@ -310,11 +291,10 @@ class DeviceGA:
             overlap()
         copied.synchronize()
         packed = packed_h.numpy()
-        vals = self._check_summary(None if summary is None else packed[n + k:].view(np.float64))
         self._mark("hof_prepare", sub=True)
         rank_np = (packed[:n] & 0xFFFFFFFF).astype(np.int32)
         cls_np = packed[:n] >> 32
-        src, new_fit = D.hof_update(self.H, self._hof_fit_host, cls_np[:old_n], packed[n:n + k].view(np.float64),
+        src, new_fit = D.hof_update(self.H, self._hof_fit_host, cls_np[:old_n], packed[n:].view(np.float64),
                                     cls_np[old_n:], rank=rank_np)
         self._mark("hof_scan", sub=True)
         m = src.shape[0]
@@ -330,21 +310,13 @@ class DeviceGA:
         self.hof_fitness[:m] = up_d[: 2 * m].view(torch.float64)
         self.hof_n = int(m)
         self._hof_fit_host = new_fit
-        return vals
 
     @staticmethod
-    def _summary(fit: torch.Tensor, invalid: torch.Tensor) -> torch.Tensor:
-        """The generation's host-side needs as one f64 device vector: whether
-        any fitness is NaN, the logbook statistics and nevals (read on the host
-        with the hall-of-fame scan's inputs, ``_check_summary``)."""
-        return torch.stack([torch.isnan(fit).any().double(), fit.mean(), fit.std(unbiased=False), fit.min(),
-                            fit.max(), invalid.sum().double()])
-
-    @staticmethod
-    def _check_summary(v):
-        if v is None:
-            return None
-        v = v.tolist()
+    def _summary(fit: torch.Tensor, invalid: torch.Tensor):
+        """One device->host sync for the generation's host-side needs: whether
+        any fitness is NaN, the logbook statistics and nevals."""
+        v = torch.stack([torch.isnan(fit).any().double(), fit.mean(), fit.std(unbiased=False), fit.min(), fit.max(),
+                         invalid.sum().double()]).tolist()
         if v[0]:
             # a NaN fitness is a game whose calculate_reward divided by zero (utils.py:106-108)
             raise ZeroDivisionError("float division by zero (calculate_reward with total_frames == 0)")
@@ -384,11 +356,11 @@ class DeviceGA:
         fit = self._evaluate(g, off, inv)  # invalid_ind only: clones keep their parent's fitness
         new_fit = torch.where(inv, fit, inherited)
         self._mark("evaluate")
+        stats, nevals = self._summary(new_fit, inv)
         # generation g + 1's parents are this offspring; its offspring go to
         # store[H:] (this generation's parents, free now), the buffer the swap
         # below makes next step's spare[H:]
-        stats, nevals = self._hof_update(new_fit, off, self.spare, summary=self._summary(new_fit, inv),
-                                         overlap=lambda: self._prefetch(g + 1, off, new_fit, self.store))
+        self._hof_update(new_fit, off, self.spare, overlap=lambda: self._prefetch(g + 1, off, new_fit, self.store))
         self._mark("hall_of_fame")
         self.fitness = new_fit
         self.store, self.spare = self.spare, self.store
@@ -428,33 +400,6 @@ class DeviceGA:
             if verbose:
                 _print_row(rows[-1], header=False)
         return rows
-
-
-def hof_ranks(member_fitness: torch.Tensor, cand_fitness: torch.Tensor) -> torch.Tensor:
-    """pg_hof_args.rank for members (HallOfFame.items order: descending
-    (fitness, age)) followed by candidates (population order, younger than
-    every member): each entry's position in ascending (fitness, age) order.
-    Equal to a stable sort of [members reversed, candidates] by fitness, but
-    only the candidates are sorted; the two ascending runs are merged with
-    searchsorted (on equal fitness the older member comes first)."""
-    old_n, k = member_fitness.shape[0], cand_fitness.shape[0]
-    ar = torch.arange(max(old_n, k), device=cand_fitness.device)
-    fcs, oc = torch.sort(cand_fitness, stable=True)
-    m_asc = member_fitness.flip(0)
-    rank_c = torch.empty(k, dtype=torch.int64, device=cand_fitness.device)
-    rank_c[oc] = ar[:k] + torch.searchsorted(m_asc, fcs, right=True)
-    rank_m = (ar[:old_n] + torch.searchsorted(fcs, m_asc, right=False)).flip(0)
-    return torch.cat([rank_m, rank_c])
-
-
-def dense_classes(hashes: torch.Tensor) -> torch.Tensor:
-    """torch.unique(hashes, return_inverse=True)[1] -- each hash's rank among
-    the distinct hashes -- from one sort and a running count, without the host
-    sync unique needs to size its output."""
-    hs, hp = torch.sort(hashes)
-    cls = torch.empty(hashes.shape[0], dtype=torch.int64, device=hashes.device)
-    cls[hp] = torch.cumsum(torch.cat([hs[:1] != hs[:1], hs[1:] != hs[:-1]]), 0)
-    return cls
 
 
 def _print_row(rec: dict, header: bool):

@@ -93,33 +93,3 @@ def test_hof_update_large_is_fast():
     assert time.perf_counter() - t0 < 1.0
     random.seed(0)
 
-
-@pytest.mark.parametrize("seed", range(8))
-def test_device_prepare_feeds_scan_like_deap(Ind, seed):
-    """DeviceGA._hof_update's prepare (evolve.hof_ranks: the merged ranks;
-    evolve.dense_classes: unique's inverse without its sync), run with torch on
-    the CPU, feeds the scan the same inputs as the full stable sort and
-    torch.unique did -- and the scan still equals DEAP's HallOfFame."""
-    import torch
-    from pong_amd.evolve import dense_classes, hof_ranks
-    rng = np.random.default_rng(100 + seed)
-    maxsize = int(rng.integers(1, 24))
-    hof = tools.HallOfFame(maxsize)
-    keys_f, keys_h = np.zeros(0), np.zeros(0, np.int64)
-    for _ in range(6):
-        n = int(rng.integers(1, 60))
-        fit = rng.integers(-4, 4, size=n).astype(np.float64) * 0.5
-        fit[rng.integers(0, n)] = -0.0  # -0.0 ties 0.0 in both orders
-        hsh = rng.integers(-2**62, 2**62, size=8)[rng.integers(0, 8, size=n)]
-        hof.update([_mk(Ind, h, f) for h, f in zip(hsh, fit)])
-        old_n = keys_f.shape[0]
-        rank = hof_ranks(torch.from_numpy(keys_f.copy()), torch.from_numpy(fit)).numpy()
-        assert np.array_equal(rank, _ranks(keys_f, fit))
-        hashes = torch.from_numpy(np.concatenate([keys_h, hsh]).astype(np.int64))
-        cls = dense_classes(hashes).numpy()
-        assert np.array_equal(cls, torch.unique(hashes, return_inverse=True)[1].numpy())
-        src, new_fit = D.hof_update(maxsize, keys_f, cls[:old_n], fit, cls[old_n:], rank=rank.astype(np.int32))
-        new_h = np.array([keys_h[s] if s < old_n else hsh[s - old_n] for s in src], dtype=np.int64)
-        assert [i.fitness.values[0] for i in hof] == list(new_fit)
-        assert [i[0] for i in hof] == list(new_h)
-        keys_f, keys_h = new_fit, new_h
