@@ -93,3 +93,46 @@ def test_hof_update_large_is_fast():
     assert time.perf_counter() - t0 < 1.0
     random.seed(0)
 
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_hof_update_merge_path_larger(Ind, seed):
+    """The merge path (members in items order, as DeviceGA always passes them)
+    over larger halls and populations, full and filling, many ties and
+    duplicates, against DEAP's HallOfFame."""
+    rng = np.random.default_rng(1000 + seed)
+    maxsize = int(rng.integers(1, 300))
+    hof = tools.HallOfFame(maxsize)
+    keys_f, keys_h = np.zeros(0), np.zeros(0, np.int64)
+    genes = rng.integers(-2**62, 2**62, size=int(rng.integers(2, 400)))
+    for _ in range(5):
+        n = int(rng.integers(0, 600))
+        fit = np.round(rng.standard_normal(n) * 2, int(rng.integers(0, 3)))
+        hsh = genes[rng.integers(0, genes.size, size=n)]
+        hof.update([_mk(Ind, h, f) for h, f in zip(hsh, fit)])
+        src, new_fit = D.hof_update(maxsize, keys_f, keys_h, fit, hsh,
+                                    rank=_ranks(keys_f, fit) if seed % 2 else None)
+        old_n = keys_f.shape[0]
+        new_h = np.array([keys_h[s] if s < old_n else hsh[s - old_n] for s in src], dtype=np.int64)
+        assert [i.fitness.values[0] for i in hof] == list(new_fit)
+        assert [i[0] for i in hof] == list(new_h)
+        keys_f, keys_h = new_fit, new_h
+
+
+def test_hof_update_general_path_unordered_members():
+    """Members not in items order take the general (full rank bitmap) path:
+    with distinct fitness the result equals the ordered call's, up to the
+    members' permutation."""
+    rng = np.random.default_rng(7)
+    H = 64
+    mf = rng.permutation(np.arange(H, dtype=np.float64))  # distinct, unordered
+    mh = rng.integers(-2**62, 2**62, size=H)
+    pf = rng.standard_normal(200) * 40 + 30
+    ph = rng.integers(-2**62, 2**62, size=200)
+    ph[::7] = mh[rng.integers(0, H, size=ph[::7].size)]  # some similar to members
+    src_u, fit_u = D.hof_update(H, mf, mh, pf, ph)
+    perm = np.argsort(-mf, kind="stable")  # items order
+    src_o, fit_o = D.hof_update(H, mf[perm], mh[perm], pf, ph)
+    assert list(fit_u) == list(fit_o)
+    back = np.array([perm[s] if s < H else s for s in src_o])
+    assert list(src_u) == list(back)
