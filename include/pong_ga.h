@@ -290,6 +290,25 @@ typedef struct pg_hof_args {
   double *new_fitness;           /* out [maxsize] */
 } pg_hof_args;
 
+/* Device half of the hall-of-fame update (pg_hof_rank_classes): for the old
+ * members (items order) and k candidate rows, each entry's pg_hof_args.rank and
+ * a dense similarity class of the row hashes, packed as
+ * packed[e] = rank[e] | class[e] << 32 for e < hof_n + k (members first), then
+ * packed[hof_n + k + j] = the bits of candidate j's fitness.  All pointers are
+ * device memory on the stream's device; workspace >=
+ * pg_hof_rank_classes_workspace_bytes(hof_n + k). */
+typedef struct pg_hof_rank_args {
+  int32_t hof_n;
+  const double *hof_fitness;     /* [hof_n] device, items order */
+  const uint64_t *hof_hash;      /* [hof_n] device */
+  int32_t k;
+  const double *cand_fitness;    /* [k] device, population order */
+  const uint64_t *cand_hash;     /* [k] device */
+  int64_t *packed;               /* out [hof_n + 2k] device */
+  void *workspace;
+  size_t workspace_bytes;
+} pg_hof_rank_args;
+
 const char *pg_version(void);
 int32_t pg_abi_version(void);
 const char *pg_last_error(void);
@@ -320,6 +339,8 @@ int32_t pg_row_hash(const void *rows, int64_t stride, const int32_t *index, int3
                     int32_t dtype, uint64_t *hash, void *stream);
 /* Host only (no device memory, no GPU needed). */
 int32_t pg_hof_update(const pg_hof_args *args);
+size_t pg_hof_rank_classes_workspace_bytes(int32_t n);
+int32_t pg_hof_rank_classes(const pg_hof_rank_args *args, void *stream);
 /* dst row j = old_rows[src[j]] if src[j] < n_old, else rows[index[src[j] - n_old]]
  * (index NULL: rows[src[j] - n_old]) -- pg_hof_update's new_src applied in one
  * pass; strides in elements, dst disjoint from both sources. */

@@ -107,6 +107,14 @@ class PgHofArgs(ctypes.Structure):
     ]
 
 
+class PgHofRankArgs(ctypes.Structure):
+    _fields_ = [
+        ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("hof_hash", _vp), ("k", ctypes.c_int32),
+        ("cand_fitness", _vp), ("cand_hash", _vp), ("packed", _vp), ("workspace", _vp),
+        ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 # name -> (restype, argtypes); exactly the functions include/pong_ga.h declares
 SIGNATURES = {
     "pg_version": (ctypes.c_char_p, []),
@@ -127,6 +135,8 @@ SIGNATURES = {
     "pg_row_hash": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp,
                                      _vp]),
     "pg_hof_update": (ctypes.c_int32, [ctypes.POINTER(PgHofArgs)]),
+    "pg_hof_rank_classes_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "pg_hof_rank_classes": (ctypes.c_int32, [ctypes.POINTER(PgHofRankArgs), _vp]),
     "pg_gather_rows": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, _vp,
                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp]),
     "pg_render_frames": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp]),

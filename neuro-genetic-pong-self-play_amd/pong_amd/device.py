@@ -398,6 +398,30 @@ def gather_rows(dst: torch.Tensor, old_rows: torch.Tensor, rows: torch.Tensor, s
     return dst
 
 
+def hof_rank_classes(hof_fitness: torch.Tensor, hof_hash: torch.Tensor, cand_fitness: torch.Tensor,
+                     cand_hash: torch.Tensor) -> torch.Tensor:
+    """pg_hof_rank_classes: the packed scan input of HallOfFame.update on the
+    device -- int64 [n + k] (n = members + k candidates): rank | class << 32 per
+    entry (members in items order first), then the candidates' fitness bits."""
+    dev = cand_fitness.device
+    hn, k = hof_fitness.shape[0], cand_fitness.shape[0]
+    _need(hof_fitness, "hof_fitness", torch.float64, dev, (hn,))
+    _need(hof_hash, "hof_hash", torch.int64, dev, (hn,))
+    _need(cand_fitness, "cand_fitness", torch.float64, dev, (k,))
+    _need(cand_hash, "cand_hash", torch.int64, dev, (k,))
+    packed = torch.empty(hn + 2 * k, dtype=torch.int64, device=dev)
+    nbytes = int(L.lib().pg_hof_rank_classes_workspace_bytes(hn + k))
+    if nbytes == 0:
+        msg = L.lib().pg_last_error()
+        raise L.PongGAError("pg_hof_rank_classes_workspace_bytes", -1, msg.decode() if msg else "")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a = L.PgHofRankArgs(hn, _ptr(hof_fitness), _ptr(hof_hash), k, _ptr(cand_fitness), _ptr(cand_hash),
+                        _ptr(packed), _ptr(ws), nbytes)
+    with torch.cuda.device(dev):
+        L.check("pg_hof_rank_classes", L.lib().pg_hof_rank_classes(ctypes.byref(a), _stream(dev)))
+    return packed
+
+
 def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash, rank=None):
     """pg_hof_update (host, no GPU): HallOfFame.update over fitness/hash arrays.
 
