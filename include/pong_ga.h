@@ -36,6 +36,8 @@
  *                                for a whole population, on device
  * pg_row_hash                    DEAP HallOfFame's similar (operator.eq on the
  *                                gene lists, ga.py:78) as a 64-bit row hash
+ * pg_hof_rank_classes            HallOfFame.update's device half: the (fitness, age)
+ *                                ranks and similarity classes the host scan reads
  * pg_hof_update (host)           tools.HallOfFame.update (eaSimple, main.py:165-170)
  * pg_gather_rows                 the new hall's genomes (HallOfFame.insert's deepcopy)
  * pg_render_frames               the frame env.step returns (main.py:77; the build's
