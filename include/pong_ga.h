@@ -36,8 +36,9 @@
  *                                for a whole population, on device
  * pg_row_hash                    DEAP HallOfFame's similar (operator.eq on the
  *                                gene lists, ga.py:78) as a 64-bit row hash
- * pg_hof_rank_classes            HallOfFame.update's device half: the (fitness, age)
- *                                ranks and similarity classes the host scan reads
+ * pg_hof_prepare /               HallOfFame.update's device half: the candidates,
+ * pg_hof_rank_classes            their hashes, the (fitness, age) ranks and
+ *                                similarity classes the host scan reads
  * pg_hof_update (host)           tools.HallOfFame.update (eaSimple, main.py:165-170)
  * pg_gather_rows                 the new hall's genomes (HallOfFame.insert's deepcopy)
  * pg_render_frames               the frame env.step returns (main.py:77; the build's
@@ -311,6 +312,32 @@ typedef struct pg_hof_rank_args {
   size_t workspace_bytes;
 } pg_hof_rank_args;
 
+/* The whole device half of the hall-of-fame update (pg_hof_prepare): the
+ * candidates (every row, or with filter the rows whose fitness is strictly
+ * above worst -- a full hall's admission rule), their row hashes, and the
+ * pg_hof_rank_classes packing of members + candidates.  One host sync (the
+ * candidate count, written to *k).  Device pointers on the stream's device;
+ * workspace >= pg_hof_prepare_workspace_bytes(hof_n, pop_n). */
+typedef struct pg_hof_prepare_args {
+  const double *fitness;         /* [pop_n] device, population order */
+  int32_t pop_n;
+  int32_t filter;                /* 1: candidates are fitness > worst; 0: every row */
+  double worst;
+  const void *rows;              /* [pop_n, stride] device, dtype */
+  int64_t stride;
+  int64_t genes;
+  int32_t dtype;
+  int32_t hof_n;
+  const double *hof_fitness;     /* [hof_n] device, items order */
+  const uint64_t *hof_hash;      /* [hof_n] device */
+  int32_t *k;                    /* out (host): number of candidates */
+  int64_t *cand;                 /* out [pop_n] device: candidate rows, population order */
+  uint64_t *hashes;              /* out [hof_n + pop_n] device: members', then candidates' hashes */
+  int64_t *packed;               /* out [hof_n + 2 pop_n] device: as pg_hof_rank_classes (n = hof_n + k) */
+  void *workspace;
+  size_t workspace_bytes;
+} pg_hof_prepare_args;
+
 const char *pg_version(void);
 int32_t pg_abi_version(void);
 const char *pg_last_error(void);
@@ -343,6 +370,8 @@ int32_t pg_row_hash(const void *rows, int64_t stride, const int32_t *index, int3
 int32_t pg_hof_update(const pg_hof_args *args);
 size_t pg_hof_rank_classes_workspace_bytes(int32_t n);
 int32_t pg_hof_rank_classes(const pg_hof_rank_args *args, void *stream);
+size_t pg_hof_prepare_workspace_bytes(int32_t hof_n, int32_t pop_n);
+int32_t pg_hof_prepare(const pg_hof_prepare_args *args, void *stream);
 /* dst row j = old_rows[src[j]] if src[j] < n_old, else rows[index[src[j] - n_old]]
  * (index NULL: rows[src[j] - n_old]) -- pg_hof_update's new_src applied in one
  * pass; strides in elements, dst disjoint from both sources. */

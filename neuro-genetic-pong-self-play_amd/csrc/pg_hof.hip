@@ -9,6 +9,8 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "pg_eval.hpp"
 
@@ -69,6 +71,26 @@ __global__ void k_hof_pack(const int32_t *rank, const int32_t *hash_order, const
 // rank[e] must be written before k_hof_pack reads it at a permuted index, so
 // the pack runs as its own launch after k_hof_rank (stream order).
 
+struct Above {  // the full hall's admission filter: fitness strictly above its worst
+  const double *fitness;
+  double worst;
+  __device__ bool operator()(int32_t i) const { return fitness[i] > worst; }
+};
+
+__global__ void k_hof_iota(int32_t *out, int n) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) out[i] = i;
+}
+
+__global__ void k_hof_cand_gather(const int32_t *cand32, int k, const double *fitness, int64_t *cand,
+                                  double *cand_fitness) {
+  const int j = blockIdx.x * kThreads + threadIdx.x;
+  if (j >= k) return;
+  const int i = cand32[j];
+  cand[j] = i;
+  cand_fitness[j] = fitness[i];
+}
+
 struct Layout {
   size_t keys_a, keys_b, iota, order, rank, flag, cls, temp, total;
   size_t temp_bytes;
@@ -105,6 +127,63 @@ int32_t layout_for(int n, Layout *L) {
   return PG_OK;
 }
 
+int32_t rank_classes_core(int hn, const double *hof_fitness, const uint64_t *hof_hash, int k,
+                          const double *cand_fitness, const uint64_t *cand_hash, int64_t *packed, char *ws,
+                          const Layout &L, hipStream_t s) {
+  const int n = hn + k;
+  double *fkeys = (double *)(ws + L.keys_a), *fsorted = (double *)(ws + L.keys_b);
+  uint64_t *hkeys = (uint64_t *)(ws + L.keys_a), *hsorted = (uint64_t *)(ws + L.keys_b);
+  int32_t *iota = (int32_t *)(ws + L.iota), *order = (int32_t *)(ws + L.order);
+  int32_t *rank = (int32_t *)(ws + L.rank), *flag = (int32_t *)(ws + L.flag), *cls = (int32_t *)(ws + L.cls);
+  void *temp = ws + L.temp;
+  size_t temp_bytes = L.temp_bytes;
+  const unsigned g = blocks_for(n);
+  // ranks: radix sort is stable, so equal fitness keeps age order
+  hipLaunchKernelGGL(k_hof_age_keys, dim3(g), dim3(kThreads), 0, s, hof_fitness, hn, cand_fitness, k, fkeys, iota);
+  PG_HIP(rocprim::radix_sort_pairs(temp, temp_bytes, fkeys, fsorted, iota, order, (unsigned)n, 0, 64, s));
+  hipLaunchKernelGGL(k_hof_rank, dim3(g), dim3(kThreads), 0, s, order, hn, n, rank);
+  // classes: sort the hashes, count the distinct values in sorted order
+  hipLaunchKernelGGL(k_hof_hash_keys, dim3(g), dim3(kThreads), 0, s, hof_hash, hn, cand_hash, k, hkeys, iota);
+  temp_bytes = L.temp_bytes;
+  PG_HIP(rocprim::radix_sort_pairs(temp, temp_bytes, hkeys, hsorted, iota, order, (unsigned)n, 0, 64, s));
+  hipLaunchKernelGGL(k_hof_new_class, dim3(g), dim3(kThreads), 0, s, hsorted, n, flag);
+  temp_bytes = L.temp_bytes;
+  PG_HIP(rocprim::inclusive_scan(temp, temp_bytes, flag, cls, (size_t)n, rocprim::plus<int32_t>(), s));
+  hipLaunchKernelGGL(k_hof_pack, dim3(blocks_for(n > k ? n : k)), dim3(kThreads), 0, s, rank, order, cls, n,
+                     cand_fitness, k, packed);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+// pg_hof_prepare's workspace: the rank/class layout for hof_n + pop_n entries,
+// then the candidate list, their fitness, the device count and select's storage.
+struct PrepLayout {
+  Layout rc;
+  size_t cand32, cfit, count, sel, total, sel_bytes;
+};
+
+int32_t prep_layout_for(int hn, int pn, const double *fitness, PrepLayout *P) {
+  if (layout_for(hn + pn, &P->rc) != PG_OK) return PG_ERR_HIP;
+  size_t sel = 0;
+  if (rocprim::select(nullptr, sel, rocprim::counting_iterator<int32_t>(0), (int32_t *)nullptr, (int32_t *)nullptr,
+                      (size_t)(pn > 0 ? pn : 1), Above{fitness, 0.0}) != hipSuccess)
+    return fail(PG_ERR_HIP, "hof_prepare: rocPRIM select storage query failed");
+  size_t off = P->rc.total;
+  auto take = [&](size_t bytes) {
+    const size_t at = off;
+    off += align_up(bytes);
+    return at;
+  };
+  const size_t pp = (size_t)(pn > 0 ? pn : 1);
+  P->cand32 = take(pp * 4);
+  P->cfit = take(pp * 8);
+  P->count = take(8);
+  P->sel_bytes = sel > 0 ? sel : 1;
+  P->sel = take(P->sel_bytes);
+  P->total = off;
+  return PG_OK;
+}
+
 }  // namespace
 }  // namespace pg
 
@@ -130,31 +209,56 @@ int32_t pg_hof_rank_classes(const pg_hof_rank_args *a, void *stream) {
   if (layout_for(n, &L) != PG_OK) return PG_ERR_HIP;
   if (!a->workspace || a->workspace_bytes < L.total)
     return fail(PG_ERR_INVALID, "hof_rank_classes: workspace of %zu bytes needed", L.total);
+  return rank_classes_core(hn, a->hof_fitness, a->hof_hash, k, a->cand_fitness, a->cand_hash, a->packed,
+                           (char *)a->workspace, L, (hipStream_t)stream);
+}
+
+size_t pg_hof_prepare_workspace_bytes(int32_t hof_n, int32_t pop_n) {
+  PrepLayout P;
+  if (hof_n < 0 || pop_n < 0 || prep_layout_for(hof_n, pop_n, nullptr, &P) != PG_OK) return 0;
+  return P.total;
+}
+
+int32_t pg_hof_prepare(const pg_hof_prepare_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  const int hn = a->hof_n, pn = a->pop_n;
+  if (hn < 0 || pn < 0 || (long)hn + pn > 0x7fffffffL || !a->k || (hn > 0 && (!a->hof_fitness || !a->hof_hash)) ||
+      (pn > 0 && (!a->fitness || !a->rows || !a->cand || !a->hashes || !a->packed)) || a->genes < 0 ||
+      (pn > 0 && a->stride < a->genes) || (a->dtype != PG_F32 && a->dtype != PG_F64))
+    return fail(PG_ERR_INVALID, "hof_prepare: bad sizes, dtype or NULL buffers");
+  *a->k = 0;
+  if (pn == 0) return PG_OK;
+  PrepLayout P;
+  if (prep_layout_for(hn, pn, a->fitness, &P) != PG_OK) return PG_ERR_HIP;
+  if (!a->workspace || a->workspace_bytes < P.total)
+    return fail(PG_ERR_INVALID, "hof_prepare: workspace of %zu bytes needed", P.total);
   char *ws = (char *)a->workspace;
-  double *fkeys = (double *)(ws + L.keys_a), *fsorted = (double *)(ws + L.keys_b);
-  uint64_t *hkeys = (uint64_t *)(ws + L.keys_a), *hsorted = (uint64_t *)(ws + L.keys_b);
-  int32_t *iota = (int32_t *)(ws + L.iota), *order = (int32_t *)(ws + L.order);
-  int32_t *rank = (int32_t *)(ws + L.rank), *flag = (int32_t *)(ws + L.flag), *cls = (int32_t *)(ws + L.cls);
-  void *temp = ws + L.temp;
-  size_t temp_bytes = L.temp_bytes;
+  int32_t *cand32 = (int32_t *)(ws + P.cand32), *count = (int32_t *)(ws + P.count);
+  double *cfit = (double *)(ws + P.cfit);
   const hipStream_t s = (hipStream_t)stream;
-  const unsigned g = blocks_for(n);
-  // ranks: radix sort is stable, so equal fitness keeps age order
-  hipLaunchKernelGGL(k_hof_age_keys, dim3(g), dim3(kThreads), 0, s, a->hof_fitness, hn, a->cand_fitness, k, fkeys,
-                     iota);
-  PG_HIP(rocprim::radix_sort_pairs(temp, temp_bytes, fkeys, fsorted, iota, order, (unsigned)n, 0, 64, s));
-  hipLaunchKernelGGL(k_hof_rank, dim3(g), dim3(kThreads), 0, s, order, hn, n, rank);
-  // classes: sort the hashes, count the distinct values in sorted order
-  hipLaunchKernelGGL(k_hof_hash_keys, dim3(g), dim3(kThreads), 0, s, a->hof_hash, hn, a->cand_hash, k, hkeys, iota);
-  temp_bytes = L.temp_bytes;
-  PG_HIP(rocprim::radix_sort_pairs(temp, temp_bytes, hkeys, hsorted, iota, order, (unsigned)n, 0, 64, s));
-  hipLaunchKernelGGL(k_hof_new_class, dim3(g), dim3(kThreads), 0, s, hsorted, n, flag);
-  temp_bytes = L.temp_bytes;
-  PG_HIP(rocprim::inclusive_scan(temp, temp_bytes, flag, cls, (size_t)n, rocprim::plus<int32_t>(), s));
-  hipLaunchKernelGGL(k_hof_pack, dim3(blocks_for(n > k ? n : k)), dim3(kThreads), 0, s, rank, order, cls, n,
-                     a->cand_fitness, k, a->packed);
-  PG_HIP(hipGetLastError());
-  return PG_OK;
+  int k = pn;
+  if (a->filter) {
+    size_t sel_bytes = P.sel_bytes;
+    PG_HIP(rocprim::select(ws + P.sel, sel_bytes, rocprim::counting_iterator<int32_t>(0), cand32, count, (size_t)pn,
+                           Above{a->fitness, a->worst}, s));
+    int32_t k_host = 0;
+    PG_HIP(hipMemcpyAsync(&k_host, count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    PG_HIP(hipStreamSynchronize(s));  // the one sync: the scan's input size
+    k = k_host;
+  } else {
+    hipLaunchKernelGGL(k_hof_iota, dim3(blocks_for(pn)), dim3(kThreads), 0, s, cand32, pn);
+  }
+  *a->k = k;
+  if (k == 0) return PG_OK;
+  if (hn > 0) PG_HIP(hipMemcpyAsync(a->hashes, a->hof_hash, (size_t)hn * 8, hipMemcpyDeviceToDevice, s));
+  const int32_t rc = pg_row_hash(a->rows, a->stride, cand32, k, a->genes, a->dtype, a->hashes + hn, stream);
+  if (rc != PG_OK) return rc;
+  hipLaunchKernelGGL(k_hof_cand_gather, dim3(blocks_for(k)), dim3(kThreads), 0, s, cand32, k, a->fitness, a->cand,
+                     cfit);
+  Layout L;
+  if (layout_for(hn + k, &L) != PG_OK) return PG_ERR_HIP;
+  if (L.total > P.rc.total) return fail(PG_ERR_INVALID, "hof_prepare: rank/class layout grew with fewer entries");
+  return rank_classes_core(hn, a->hof_fitness, a->hashes, k, cfit, a->hashes + hn, a->packed, ws, L, s);
 }
 
 }  // extern "C"

@@ -115,6 +115,15 @@ class PgHofRankArgs(ctypes.Structure):
     ]
 
 
+class PgHofPrepareArgs(ctypes.Structure):
+    _fields_ = [
+        ("fitness", _vp), ("pop_n", ctypes.c_int32), ("filter", ctypes.c_int32), ("worst", ctypes.c_double),
+        ("rows", _vp), ("stride", ctypes.c_int64), ("genes", ctypes.c_int64), ("dtype", ctypes.c_int32),
+        ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("hof_hash", _vp), ("k", _vp), ("cand", _vp),
+        ("hashes", _vp), ("packed", _vp), ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 # name -> (restype, argtypes); exactly the functions include/pong_ga.h declares
 SIGNATURES = {
     "pg_version": (ctypes.c_char_p, []),
@@ -137,6 +146,8 @@ SIGNATURES = {
     "pg_hof_update": (ctypes.c_int32, [ctypes.POINTER(PgHofArgs)]),
     "pg_hof_rank_classes_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "pg_hof_rank_classes": (ctypes.c_int32, [ctypes.POINTER(PgHofRankArgs), _vp]),
+    "pg_hof_prepare_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "pg_hof_prepare": (ctypes.c_int32, [ctypes.POINTER(PgHofPrepareArgs), _vp]),
     "pg_gather_rows": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, _vp,
                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp]),
     "pg_render_frames": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp]),

@@ -422,6 +422,38 @@ def hof_rank_classes(hof_fitness: torch.Tensor, hof_hash: torch.Tensor, cand_fit
     return packed
 
 
+def hof_prepare(fitness: torch.Tensor, worst: Optional[float], rows: torch.Tensor, genes: int,
+                hof_fitness: torch.Tensor, hof_hash: torch.Tensor):
+    """pg_hof_prepare: the device half of HallOfFame.update in one call.
+    Candidates are every row (worst None) or the rows with fitness > worst.
+    Returns (k, cand [k] int64 rows, hashes [hof_n + k] int64, packed
+    [hof_n + 2k] int64 as hof_rank_classes); one host sync (k)."""
+    dev = fitness.device
+    pn, hn = fitness.shape[0], hof_fitness.shape[0]
+    _need(fitness, "fitness", torch.float64, dev, (pn,))
+    _need(hof_fitness, "hof_fitness", torch.float64, dev, (hn,))
+    _need(hof_hash, "hof_hash", torch.int64, dev, (hn,))
+    if rows.dim() != 2 or rows.shape[0] != pn or rows.dtype not in DTYPES or rows.stride(1) != 1 or rows.device != dev:
+        raise ValueError("rows must be a row-major [pop_n, G] f32/f64 tensor on fitness's device")
+    cand = torch.empty(pn, dtype=torch.int64, device=dev)
+    hashes = torch.empty(hn + pn, dtype=torch.int64, device=dev)
+    packed = torch.empty(hn + 2 * pn, dtype=torch.int64, device=dev)
+    nbytes = int(L.lib().pg_hof_prepare_workspace_bytes(hn, pn))
+    if nbytes == 0:
+        msg = L.lib().pg_last_error()
+        raise L.PongGAError("pg_hof_prepare_workspace_bytes", -1, msg.decode() if msg else "")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    k = ctypes.c_int32(0)
+    stride = rows.stride(0) if pn > 1 else rows.shape[1]
+    a = L.PgHofPrepareArgs(_ptr(fitness), pn, 0 if worst is None else 1, 0.0 if worst is None else float(worst),
+                           _ptr(rows), stride, int(genes), DTYPES[rows.dtype], hn, _ptr(hof_fitness), _ptr(hof_hash),
+                           ctypes.addressof(k), _ptr(cand), _ptr(hashes), _ptr(packed), _ptr(ws), nbytes)
+    with torch.cuda.device(dev):
+        L.check("pg_hof_prepare", L.lib().pg_hof_prepare(ctypes.byref(a), _stream(dev)))
+    k = k.value
+    return k, cand[:k], hashes[: hn + k], packed[: hn + 2 * k]
+
+
 def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash, rank=None):
     """pg_hof_update (host, no GPU): HallOfFame.update over fitness/hash arrays.
 

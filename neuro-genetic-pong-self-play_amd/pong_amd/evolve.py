@@ -95,9 +95,9 @@ class DeviceGA:
         # only: every game's result is the same in any order.
         self.order_by_length = True
         self.lineage_frames = torch.zeros(self.P, dtype=torch.float32, device=self.device)
-        # hall-of-fame ranks and classes by pg_hof_rank_classes (one native call,
-        # measured 0.15 ms faster per generation at pop 65 536); False: the same
-        # scan input from torch ops (stable sort + unique), kept as the cross-check
+        # the hall-of-fame update's device half by pg_hof_prepare (one native call:
+        # candidates, hashes, ranks, classes); False: the same scan input from
+        # torch ops (nonzero, stable sort, unique), kept as the cross-check
         self.native_prepare = True
 
     # ------------------------------------------------------------ views
@@ -258,20 +258,23 @@ class DeviceGA:
                 overlap()
             return
         old_n = self.hof_n
-        if old_n >= self.H:
-            # a full hall only admits fitness > its worst, and the worst only rises:
-            # rows at or below today's worst can never enter
-            cand = torch.nonzero(fit > float(self._hof_fit_host[-1])).flatten()
+        # a full hall only admits fitness > its worst, and the worst only rises:
+        # rows at or below today's worst can never enter
+        worst = float(self._hof_fit_host[-1]) if old_n >= self.H else None
+        if self.native_prepare:  # pg_hof_prepare: candidates, hashes, ranks, classes in one call
+            k, cand, hashes, packed_d = D.hof_prepare(fit, worst, rows, self.G, self.hof_fitness[:old_n],
+                                                      self.hof_hash[:old_n])
+        elif worst is not None:
+            cand = torch.nonzero(fit > worst).flatten()
         else:
             cand = torch.arange(self.P, device=self.device)
-        k = int(cand.numel())
+        if not self.native_prepare:
+            k = int(cand.numel())
         if k == 0:
             dst[:old_n] = self.store[:old_n]
             if overlap:
                 overlap()
             return
-        h = D.row_hash(rows, self.G, index=cand.to(torch.int32))
-        fc = fit[cand]
         # Everything the sequential scan needs, computed on the device and sent
         # in one copy: each entry's rank in ascending (fitness, age) order (in
         # age order the old members come oldest first, then the candidates), a
@@ -279,10 +282,10 @@ class DeviceGA:
         n = old_n + k
         if self.profile is not None:
             self.profile["hof_candidates"] = self.profile.get("hof_candidates", 0) + k
-        hashes = torch.cat([self.hof_hash[:old_n], h])
-        if self.native_prepare:  # pg_hof_rank_classes: one call, no host sync
-            packed_d = D.hof_rank_classes(self.hof_fitness[:old_n], hashes[:old_n], fc, hashes[old_n:])
-        else:
+        if not self.native_prepare:
+            h = D.row_hash(rows, self.G, index=cand.to(torch.int32))
+            fc = fit[cand]
+            hashes = torch.cat([self.hof_hash[:old_n], h])
             by_age = torch.cat([self.hof_fitness[:old_n].flip(0), fc])
             order = torch.sort(by_age, stable=True).indices
             rank_age = torch.empty_like(order)

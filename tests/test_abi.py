@@ -115,7 +115,7 @@ def test_struct_layout_matches_c(tmp_path):
     structs = {"pg_net": _lib.PgNet, "pg_eval_args": _lib.PgEvalArgs, "pg_forward_args": _lib.PgForwardArgs,
                "pg_ga_args": _lib.PgGaArgs, "pg_select_args": _lib.PgSelectArgs,
                "pg_schedule_args": _lib.PgScheduleArgs, "pg_hof_args": _lib.PgHofArgs,
-               "pg_hof_rank_args": _lib.PgHofRankArgs}
+               "pg_hof_rank_args": _lib.PgHofRankArgs, "pg_hof_prepare_args": _lib.PgHofPrepareArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -80,3 +80,36 @@ def test_device_ga_native_prepare_same_run(gpu, pop):
     a, b = runs
     assert torch.equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]) and a[4] == b[4]
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("pop,old_n,filtered", [(1, 0, False), (500, 0, False), (3000, 700, True),
+                                                 (65536, 16384, True), (4000, 1000, True)])
+def test_prepare_matches_torch_path(gpu, dtype, pop, old_n, filtered):
+    """pg_hof_prepare = nonzero(fitness > worst) + pg_row_hash + the torch
+    ranks/classes: same candidates, hashes and ranks, same partition."""
+    from pong_amd import device as D
+    rng = np.random.default_rng(pop + old_n)
+    G = 37
+    rows = torch.from_numpy(rng.standard_normal((pop, G))).to(gpu, dtype)
+    rows[1::9] = rows[0]  # duplicate rows -> equal hashes
+    fit = torch.from_numpy(np.round(rng.standard_normal(pop), 1)).to(gpu)
+    hf = torch.from_numpy(np.sort(np.round(rng.standard_normal(old_n), 1))[::-1].copy()).to(gpu)
+    hh = D.row_hash(torch.from_numpy(rng.standard_normal((max(old_n, 1), G))).to(gpu, dtype), G)[:old_n]
+    if old_n > 3:
+        hh[3] = D.row_hash(rows[:1], G)[0]  # a member similar to some candidates
+    worst = float(hf[-1]) if filtered else None
+    k, cand, hashes, packed = D.hof_prepare(fit, worst, rows, G, hf, hh)
+    want = torch.nonzero(fit > worst).flatten() if filtered else torch.arange(pop, device=gpu)
+    assert k == want.numel() and torch.equal(cand, want)
+    if k == 0:
+        return
+    h = D.row_hash(rows, G, index=want.to(torch.int32))
+    assert torch.equal(hashes, torch.cat([hh, h]))
+    ref = _torch_packed(hf, hh, fit[want], h).cpu().numpy()
+    got = packed.cpu().numpy()
+    n = old_n + k
+    assert np.array_equal(got[:n] & 0xFFFFFFFF, ref[:n] & 0xFFFFFFFF) and np.array_equal(got[n:], ref[n:])
+    allh = hashes.cpu().numpy()
+    nu = np.unique(allh).size
+    assert np.unique(np.stack([got[:n] >> 32, allh]), axis=1).shape[1] == nu == np.unique(got[:n] >> 32).size
