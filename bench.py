@@ -379,10 +379,12 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
     workers = args.cpu_threads
     # numpy loop on `workers` processes, then on one core (~secs and ~secs/2 of wall time)
     np_rows = min(n, per_worker * workers)
-    rate_p, steps_p, games_p, dt_p = NL.timed_rate(shape, genomes[:np_rows], k[:np_rows], o[:np_rows],
-                                                   m[:np_rows], opponents, secs, workers, pool)
-    rate_1, steps_1, games_1, dt_1 = NL.timed_rate(shape, genomes[:8], k[:8], o[:8], m[:8], opponents,
-                                                   secs / 2, 1)
+    # the one-core leg: worker 0's own games replayed alone in one pool process
+    # afterwards (the same sample from its start, nothing else running)
+    rate_p, steps_p, games_p, dt_p, solo = NL.timed_rate(shape, genomes[:np_rows], k[:np_rows], o[:np_rows],
+                                                         m[:np_rows], opponents, secs, workers, pool,
+                                                         solo_seconds=secs / 2)
+    rate_1, steps_1, games_1, dt_1, w0_pooled = solo
     # the C restatement with OpenMP
     steps, done = 0, 0
     t0 = time.perf_counter()
@@ -397,7 +399,9 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
                       f"one BLAS thread each: {games_p} whole games of the same workload's first genomes "
                       f"({steps_p} env-steps; each worker timed on its own clock, at most {dt_p:.1f} s; value = "
                       f"the sum of the workers' rates); {workers} = this box's CPU share per GPU",
-            "one_core": {"value": rate_1, "sample": f"{games_1} games, {steps_1} env-steps in {dt_1:.1f} s"},
+            "one_core": {"value": rate_1, "sample": f"worker 0's games of the pooled run, replayed alone in one "
+                                                     f"process: {games_1} games, {steps_1} env-steps in {dt_1:.1f} s",
+                         "worker0_in_pool": w0_pooled},
             "calibration": "numpy_loop runs 1.11x the reference's own rate on the same games, equal rewards "
                            "(profiles/r02/cpu_calibration.json)",
             "c_port": {"value": steps / dt if dt > 0 else None, "cores": workers,

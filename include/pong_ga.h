@@ -81,7 +81,8 @@ typedef enum pg_precision {
   /* f32 hidden math with a certified f64 argmax: every decision whose
    * f32 error bound cannot prove the f64 argmax is recomputed in f64. */
   PG_PREC_CERTIFIED = 0,
-  /* every forward in f64 (numpy_nn's arithmetic, sequential sums) */
+  /* every forward in f64 (numpy_nn's arithmetic: each dot product in np.dot's own
+   * order, OpenBLAS dgemv_t's partial sums, blas_dot in pg_device.hpp) */
   PG_PREC_F64 = 1
 } pg_precision;
 

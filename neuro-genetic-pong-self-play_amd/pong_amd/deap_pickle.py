@@ -13,8 +13,10 @@ classes live at other paths.  This module bridges the two:
   restatement when deap is absent (and the restatement's own paths, written by
   older builds, to real DEAP when it is present).  It resolves only the
   globals a checkpoint can contain (the DEAP classes above, ``copyreg`` /
-  ``operator`` helpers, numpy scalars and arrays); anything else raises
-  ``pickle.UnpicklingError`` instead of importing it.
+  ``operator.eq``, numpy scalars and arrays), each by its exact
+  ``(module, name)`` pair; anything else -- any other name of an allowed
+  module, or a dotted name -- raises ``pickle.UnpicklingError`` instead of
+  importing it.
 * ``dump`` pickles restatement objects under DEAP's module paths, so the
   reference's ``ga.load_population_from_file`` (ga.py:41-53, real DEAP)
   reads the build's exports.  The C pickler resolves a class by importing its
@@ -63,8 +65,12 @@ _ALLOWED = {
     ("numpy", "dtype"), ("numpy", "ndarray"),
     ("numpy.core.multiarray", "scalar"), ("numpy.core.multiarray", "_reconstruct"),
     ("numpy._core.multiarray", "scalar"), ("numpy._core.multiarray", "_reconstruct"),
+    # HallOfFame.similar (operator.eq, ga.py:78): the only operator global a
+    # checkpoint holds.  Exact pairs, never whole modules: _operator's
+    # attrgetter / getitem / methodcaller reach eval through a reconstructor's
+    # __globals__ with GLOBAL and REDUCE alone.
+    ("_operator", "eq"), ("operator", "eq"),
 }
-_ALLOWED_MODULES = {"_operator", "operator"}  # HallOfFame.similar (operator.eq) and kin
 
 
 def deap_installed() -> bool:
@@ -95,6 +101,8 @@ class CheckpointUnpickler(pickle.Unpickler):
 
     def find_class(self, module, name):
         key = (module, name)
+        if "." in name:  # protocol 4 resolves dotted names attribute by attribute
+            raise pickle.UnpicklingError(f"checkpoint names {module}.{name}: dotted names are refused")
         if key in _DEAP_TO_COMPAT or key in _COMPAT_TO_DEAP:
             if self.use_deap:
                 module, name = _COMPAT_TO_DEAP.get(key, key)
@@ -104,7 +112,7 @@ class CheckpointUnpickler(pickle.Unpickler):
             if module.endswith("creator"):
                 _ensure_creator_classes(mod)
             return getattr(mod, name)
-        if key in _ALLOWED or module in _ALLOWED_MODULES:
+        if key in _ALLOWED:
             return super().find_class(module, name)
         raise pickle.UnpicklingError(f"checkpoint names {module}.{name}, which a save_checkpoint "
                                      "file never holds; refusing to import it")

@@ -8,7 +8,6 @@ draws the same opponents as a sequential map of evaluate() would.
 """
 import datetime
 import os
-import pickle
 import random
 from copy import deepcopy
 
@@ -17,6 +16,7 @@ import numpy as np
 from config import *  # noqa: F401,F403  (NETWORK_SHAPE etc., as the reference's utils.py:9)
 from config import GAME_PLAYABLE_HEIGHT, GAME_WIDTH, SCALED_PADDLE_HEIGHT, TIME_SCALER
 from numpy_nn import NeuralNetwork
+from pong_amd import deap_pickle
 
 
 def find_stuff(observation):
@@ -87,7 +87,12 @@ def get_random_action(all_actions):
 
 def save_checkpoint(_population, hall_of_fame):
     """Pickle {population, hall_of_fame, rndstate, network_shape} to
-    checkpoints/checkpoints/c_HH_MM_SS.pkl (utils.py:116-125 format)."""
+    checkpoints/checkpoints/c_HH_MM_SS.pkl (utils.py:116-125 format) and
+    return the path.  The pickle names DEAP's class paths
+    (``deap.creator.Individual``, ``deap.creator.Fitness``,
+    ``deap.tools.support.HallOfFame``) even when the in-repo restatement made
+    the objects, so the reference's ``ga.load_population_from_file``
+    (ga.py:41-45, plain ``pickle.load`` with real DEAP) resumes from it."""
     payload = {
         "population": _population,
         "hall_of_fame": deepcopy(hall_of_fame),
@@ -96,8 +101,10 @@ def save_checkpoint(_population, hall_of_fame):
     }
     os.makedirs("checkpoints/checkpoints", exist_ok=True)
     stamp = datetime.datetime.now().strftime("%H_%M_%S")
-    with open(os.path.join("checkpoints", "checkpoints", f"c_{stamp}.pkl"), "wb") as fh:
-        pickle.dump(payload, fh)
+    path = os.path.join("checkpoints", "checkpoints", f"c_{stamp}.pkl")
+    with open(path, "wb") as fh:
+        deap_pickle.dump(payload, fh)
+    return path
 
 
 def calculate_gene_size():

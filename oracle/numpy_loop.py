@@ -244,13 +244,19 @@ def evaluate(nodes, genes, kinds, opp_rows, mults, opponents, base_seed=0):
 def _worker(job):
     """One BLAS thread per worker: the pool is the parallelism (as SCOOP's
     worker processes are); an OpenBLAS pool per process would oversubscribe
-    the cores (16 processes x OMP_NUM_THREADS threads on the GPU box)."""
-    try:
-        from threadpoolctl import threadpool_limits
-    except ImportError:  # timing helper: run as is without it
-        return _games(job)
-    with threadpool_limits(1):
-        return _games(job)
+    the cores (16 processes x OMP_NUM_THREADS threads on the GPU box).
+    find_stuff's np.average of an absent colour warns "Mean of empty slice"
+    on every hidden-ball frame, as the reference's does; the workers do not
+    print it (the returned None is the reference's behaviour either way)."""
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        try:
+            from threadpoolctl import threadpool_limits
+        except ImportError:  # timing helper: run as is without it
+            return _games(job)
+        with threadpool_limits(1):
+            return _games(job)
 
 
 def _games(job):
@@ -285,28 +291,46 @@ def make_pool(workers):
     return mp.get_context("fork").Pool(workers)
 
 
-def timed_rate(nodes, genomes, kinds, opps, mults, opponents, seconds, workers=1, pool=None):
-    """env-steps/s of whole games (evaluate()'s perform_episode calls, in order)
-    over ``seconds`` of each worker's time, genomes dealt round-robin to
-    ``workers`` processes (as SCOOP's futures.map spreads evaluate() over
-    cores, ga.py:83), all running at once: the rate is the sum of the workers'
-    own rates (env-steps / busy seconds).  Returns (rate, env-steps, games,
-    the longest worker's busy seconds)."""
-    if workers <= 1:
-        steps, games, dt = _worker((nodes, genomes, kinds, opps, mults, opponents, seconds, 0))
-        return (steps / dt if dt > 0 else 0.0), steps, games, dt
+def _jobs(nodes, genomes, kinds, opps, mults, opponents, seconds, workers):
     jobs = []
     for w in range(workers):  # each worker gets only the opponent rows its games use
         ow = np.asarray(opps[w::workers])
         rows = np.unique(ow)
         jobs.append((nodes, genomes[w::workers], kinds[w::workers], np.searchsorted(rows, ow).astype(np.int32),
                      mults[w::workers], opponents[rows], seconds, w))
+    return jobs
+
+
+def timed_rate(nodes, genomes, kinds, opps, mults, opponents, seconds, workers=1, pool=None, solo_seconds=None):
+    """env-steps/s of whole games (evaluate()'s perform_episode calls, in order)
+    over ``seconds`` of each worker's time, genomes dealt round-robin to
+    ``workers`` processes (as SCOOP's futures.map spreads evaluate() over
+    cores, ga.py:83), all running at once: the rate is the sum of the workers'
+    own rates (env-steps / busy seconds).  Returns (rate, env-steps, games,
+    the longest worker's busy seconds).
+
+    ``solo_seconds``: also run worker 0's job ALONE afterwards (one process,
+    the same games from the start, nothing else running) -- the one-core
+    figure on the same sample as the pooled one; then returns a 5th element
+    (solo rate, solo env-steps, solo games, solo seconds, worker 0's pooled
+    rate)."""
+    jobs = _jobs(nodes, genomes, kinds, opps, mults, opponents, seconds, max(workers, 1))
+    own = None
     if pool is None:
-        with make_pool(workers) as own:
-            res = own.map(_worker, jobs)
-    else:
+        own = pool = make_pool(max(workers, 1))
+    try:
         res = pool.map(_worker, jobs)
+        solo = None
+        if solo_seconds is not None:
+            j0 = jobs[0][:6] + (solo_seconds, 0)
+            s_steps, s_games, s_dt = pool.apply(_worker, (j0,))
+            solo = ((s_steps / s_dt if s_dt > 0 else 0.0), s_steps, s_games, s_dt,
+                    (res[0][0] / res[0][2] if res[0][2] > 0 else 0.0))
+    finally:
+        if own is not None:
+            own.close()
     steps = sum(r[0] for r in res)
     games = sum(r[1] for r in res)
     rate = sum(r[0] / r[2] for r in res if r[2] > 0)
-    return rate, steps, games, max(r[2] for r in res)
+    out = (rate, steps, games, max(r[2] for r in res))
+    return out + (solo,) if solo_seconds is not None else out

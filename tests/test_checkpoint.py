@@ -193,3 +193,81 @@ def test_checkpoint_unpickler_refuses_foreign_globals():
         D.loads(pickle.dumps(os.getcwd))  # posix.getcwd: not a checkpoint global
     with pytest.raises(pickle.UnpicklingError):
         D.loads(b"cos\nsystem\n(S'true'\ntR.")
+
+
+def test_checkpoint_unpickler_refuses_operator_gadgets():
+    """Only operator.eq of the operator modules: attrgetter / getitem /
+    methodcaller reach eval through a reconstructor's __globals__ with GLOBAL
+    and REDUCE alone, and a dotted name walks attributes (protocol 4)."""
+    import pickle
+
+    import pytest
+
+    from pong_amd import deap_pickle as D
+    attr_globals = b"c_operator\nattrgetter\n(S'__globals__'\ntR(ccopyreg\n_reconstructor\ntR."
+    with pytest.raises(pickle.UnpicklingError):
+        D.loads(attr_globals)
+    getitem = (b"c_operator\ngetitem\n(c_operator\nattrgetter\n(S'__globals__'\ntR(ccopyreg\n_reconstructor\n"
+               b"tRS'__builtins__'\ntR.")
+    with pytest.raises(pickle.UnpicklingError):
+        D.loads(getitem)
+    for mod in ("_operator", "operator"):
+        for name in ("methodcaller", "itemgetter", "attrgetter", "getitem"):
+            with pytest.raises(pickle.UnpicklingError):
+                D.loads(b"c" + mod.encode() + b"\n" + name.encode() + b"\n.")
+    # a dotted name of an allowed global (STACK_GLOBAL, protocol 4)
+    dotted = b"\x80\x04\x95\x00\x00\x00\x00\x00\x00\x00\x00\x8c\x07copyreg\x8c\x1a_reconstructor.__globals__\x93."
+    with pytest.raises(pickle.UnpicklingError):
+        D.loads(dotted)
+    # what a hall of fame does hold still loads
+    import operator
+    assert D.loads(pickle.dumps(operator.eq)) is operator.eq
+
+
+def test_dropin_save_checkpoint_is_reference_readable(tmp_path):
+    """The drop-in main()'s checkpoint (utils.save_checkpoint after one
+    GENERATIONS_BEFORE_SAVE block of eaSimple at POPULATION_SIZE 64, as
+    main.py:165-173; a CPU evaluate stands in for the device map) names only
+    DEAP's classes, and a process with a DEAP-layout package and the
+    reference's plain pickle.load (ga.py:41-45) reads it back."""
+    code = ("import sys, json; sys.path.insert(0, %r); import ga, utils\n"
+            "from pong_amd.deap_compat import algorithms\n"
+            "ga.toolbox.register('evaluate', lambda ind: (sum(ind) - 0.01 * ind[0] ** 2,))\n"
+            "ga.toolbox.register('map', map)\n"
+            "pop, log = algorithms.eaSimple(ga.population, ga.toolbox, ga.CROSSOVER_BLEND_PROBABILITY,\n"
+            "    ga.GAUSSIAN_MUTATION_PROBABILITY, ga.GENERATIONS_BEFORE_SAVE, halloffame=ga.hall_of_fame,\n"
+            "    verbose=False)\n"
+            "path = utils.save_checkpoint(pop, ga.hall_of_fame)\n"
+            "print(json.dumps({'path': path, 'genes': [list(i) for i in pop], 'fit': [i.fitness.values[0] for i in pop],\n"
+            " 'hof_fit': [i.fitness.values[0] for i in ga.hall_of_fame.items], 'maxsize': ga.hall_of_fame.maxsize}))"
+            % PKG)
+    saved = _run(code, tmp_path)
+    path = os.path.join(str(tmp_path), saved["path"])
+    from pong_amd import deap_pickle as D
+    data = open(path, "rb").read()
+    names = D.global_names(data)
+    assert names <= {"deap.creator.Individual", "deap.creator.Fitness", "deap.tools.support.HallOfFame",
+                     "_operator.eq"}, names
+    assert "deap.creator.Individual" in names and "deap.tools.support.HallOfFame" in names
+    assert len(saved["genes"]) == 64 and saved["maxsize"] == 16 and len(saved["hof_fit"]) == 16
+    code = ("import sys, json, pickle; sys.path.insert(0, %r)\n"
+            "from deap import base, creator\n"
+            "creator.create('Fitness', base.Fitness, weights=(1.0,))\n"
+            "creator.create('Individual', list, fitness=creator.Fitness)\n"
+            "cp = pickle.load(open(%r, 'rb'))\n"
+            "pop, hof = cp['population'], cp['hall_of_fame']\n"
+            "print(json.dumps({'mod': type(pop[0]).__module__, 'hmod': type(hof).__module__,\n"
+            " 'genes': [list(i) for i in pop], 'fit': [i.fitness.values[0] for i in pop],\n"
+            " 'hof_fit': [i.fitness.values[0] for i in hof.items], 'maxsize': hof.maxsize,\n"
+            " 'shape': cp['network_shape'], 'rnd': cp['rndstate'][0]}))" % (STUB_DEAP, path))
+    got = _run(code, tmp_path)
+    assert got["mod"] == "deap.creator" and got["hmod"] == "deap.tools.support"
+    assert got["genes"] == saved["genes"] and got["fit"] == saved["fit"]
+    assert got["hof_fit"] == saved["hof_fit"] and got["maxsize"] == 16
+    assert got["shape"] == [6, 2, 2] and got["rnd"] == 3
+    # and the drop-in ga resumes from it (ga.py:13-29 at import: the newest checkpoint)
+    code = ("import sys, json; sys.path.insert(0, %r); import ga\n"
+            "print(json.dumps({'n': len(ga.population), 'best': ga.population[0].fitness.values[0],\n"
+            " 'hof': len(ga.hall_of_fame)}))" % PKG)
+    got = _run(code, tmp_path)
+    assert got == {"n": 64, "best": max(saved["fit"]), "hof": 16}

@@ -101,3 +101,55 @@ def test_easimple_device_equals_sequential_oracle(gpu, oracle):
     assert dev[1] == seq[1]
     assert dev[0] == seq[0]
     assert dev[2] == seq[2]
+
+
+def test_main_block_checkpoint_reference_readable(gpu, tmp_path, monkeypatch):
+    """One block of the drop-in main() (main.py:165-173: eaSimple for
+    GENERATIONS_BEFORE_SAVE generations through the device map at
+    POPULATION_SIZE 64, then save_checkpoint): the pickle names only DEAP's
+    classes and the reference's plain pickle.load, with a DEAP-layout package,
+    reads back the same population and hall of fame."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    import ga
+    import main
+    import utils
+    from pong_amd import deap_pickle as D
+    from pong_amd.deap_compat import algorithms, tools
+
+    monkeypatch.chdir(tmp_path)
+    random.seed(7)
+    pop = ga.toolbox.population(n=ga.POPULATION_SIZE)
+    hof = tools.HallOfFame(ga.HALL_OF_FAME_AMOUNT)
+    saved = main.hall_of_fame
+    try:
+        main.hall_of_fame = hof
+        stats = tools.Statistics(lambda ind: ind.fitness.values)
+        stats.register("max", np.max)
+        pop, log = algorithms.eaSimple(pop, ga.toolbox, cxpb=ga.CROSSOVER_BLEND_PROBABILITY,
+                                       mutpb=ga.GAUSSIAN_MUTATION_PROBABILITY, ngen=ga.GENERATIONS_BEFORE_SAVE,
+                                       stats=stats, halloffame=hof, verbose=False)
+        path = utils.save_checkpoint(pop, hof)
+    finally:
+        main.hall_of_fame = saved
+    names = D.global_names(open(path, "rb").read())
+    assert names <= {"deap.creator.Individual", "deap.creator.Fitness", "deap.tools.support.HallOfFame",
+                     "_operator.eq"}, names
+    stub = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "stub_deap")
+    code = ("import sys, json, pickle; sys.path.insert(0, %r)\n"
+            "from deap import base, creator\n"
+            "creator.create('Fitness', base.Fitness, weights=(1.0,))\n"
+            "creator.create('Individual', list, fitness=creator.Fitness)\n"
+            "cp = pickle.load(open(%r, 'rb'))\n"
+            "print(json.dumps({'genes': [list(i) for i in cp['population']],\n"
+            " 'fit': [i.fitness.values[0] for i in cp['population']],\n"
+            " 'hof': [i.fitness.values[0] for i in cp['hall_of_fame'].items]}))" % (stub, os.path.abspath(path)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    assert got["genes"] == [list(i) for i in pop]
+    assert got["fit"] == [i.fitness.values[0] for i in pop]
+    assert got["hof"] == [i.fitness.values[0] for i in hof.items]

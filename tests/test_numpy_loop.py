@@ -73,3 +73,19 @@ def test_timed_rate_pool():
     mult = np.ones((4, 6))
     rate, steps, games, dt = NL.timed_rate(shape, genomes, kinds, opp, mult, genomes[:1], 1.0, workers=2)
     assert steps > 0 and games > 0 and rate > 0
+
+
+def test_timed_rate_solo_leg_same_sample():
+    """The one-core leg replays worker 0's games alone: same games from the start."""
+    import numpy as np
+    import numpy_loop as NL
+    shape = [6, 2, 2]
+    rng = np.random.default_rng(5)
+    genomes = rng.standard_normal((4, 20))
+    kinds = np.zeros((4, 6), np.int32)
+    opp = np.zeros((4, 6), np.int32)
+    mult = np.ones((4, 6))
+    out = NL.timed_rate(shape, genomes, kinds, opp, mult, genomes[:1], 0.5, workers=2, solo_seconds=0.5)
+    assert len(out) == 5
+    rate_s, steps_s, games_s, dt_s, w0 = out[4]
+    assert rate_s > 0 and steps_s > 0 and games_s > 0 and w0 > 0
