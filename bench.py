@@ -135,8 +135,6 @@ def main():
     ga.set_hall_of_fame(None, np.full(H, -1e300))
     lo = ga.lo
 
-    ev_start = torch.cuda.Event(enable_timing=True)
-    ev_end = torch.cuda.Event(enable_timing=True)
     for w in range(args.warmup):
         ga.step()
     torch.cuda.synchronize(dev)
@@ -150,17 +148,17 @@ def main():
     cert_local = [0, 0, 0]  # certificate failures, decided by the service wave, decided in-wave
     passes_local = 0        # k_wide: network weight passes (each streams one network's genes once)
     skip_local = 0          # episode frames of periodic rallies not simulated (counters[8])
-    kernel_ms = []
     counters = []
-    ga.eval_events = (ev_start, ev_end)
+    events = []
     for s in range(args.steps):
+        # a fresh pair per step, read after the timed region: no per-step sync
+        ga.eval_events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        events.append(ga.eval_events)
         ga.step()  # evaluate + all-gather + hall of fame + select + vary (one generation)
         counters.append(ga.last.counters.clone())
-        # events are reused: read this step's kernel time before the next record
-        torch.cuda.synchronize(dev)
-        kernel_ms.append(ev_start.elapsed_time(ev_end))
     ga.eval_events = None
     torch.cuda.synchronize(dev)
+    kernel_ms = [a.elapsed_time(b) for a, b in events]
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)

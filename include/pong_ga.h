@@ -41,6 +41,15 @@
  *                                similarity classes the host scan reads
  * pg_hof_update (host)           tools.HallOfFame.update (eaSimple, main.py:165-170)
  * pg_gather_rows                 the new hall's genomes (HallOfFame.insert's deepcopy)
+ * pg_ga_scatter_fitness /        eaSimple's bookkeeping around toolbox.map
+ * pg_ga_merge_fitness            (main.py:165-170): fitness assigned to invalid_ind,
+ *                                clones keep their parent's, the logbook statistics
+ *                                (main.py:158-162), the hall's candidates
+ * pg_ga_select_ranked            tools.selTournament (ga.py:94) with its sort inside
+ * pg_ga_inherit / pg_ga_order    varAnd's clones' inherited state; the evaluation
+ *                                order of invalid_ind
+ * pg_hof_prepare_cand /          HallOfFame.update's device half for known
+ * pg_hof_commit                  candidates; the new members' rows, hashes, fitness
  * pg_render_frames               the frame env.step returns (main.py:77; the build's
  *                                rasteriser of its SoA state in config.py colours)
  * pg_find_stuff                  find_stuff utils.py:14-19 / get_rect_quickly
@@ -56,7 +65,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 4
+#define PG_ABI_VERSION 5
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -373,6 +382,126 @@ size_t pg_hof_rank_classes_workspace_bytes(int32_t n);
 int32_t pg_hof_rank_classes(const pg_hof_rank_args *args, void *stream);
 size_t pg_hof_prepare_workspace_bytes(int32_t hof_n, int32_t pop_n);
 int32_t pg_hof_prepare(const pg_hof_prepare_args *args, void *stream);
+/* ---- one eaSimple generation around the evaluation (DeviceGA; DEAP's eaSimple,
+ * main.py:165-170, operators ga.py:89-94).  Device pointers on the stream's
+ * device; each call is stream-ordered and syncs nothing. ---- */
+
+/* The evaluation's results in the shard's row order (toolbox.map's results
+ * assigned to invalid_ind, eaSimple): entry i (< *n_active, or every entry
+ * when n_active is NULL) played population row rows[i] (NULL: row_lo + i):
+ * shard_fitness[rows[i] - row_lo] = fitness[i] and, when lineage is given,
+ * lineage[rows[i]] = max over games of frames[i][g] (the evaluation order's
+ * prediction); shard rows no entry played read 0.  rows must be a permutation
+ * of the shard's rows. */
+typedef struct pg_scatter_args {
+  int32_t n;                     /* entries = shard rows */
+  int32_t n_games;
+  int32_t row_lo;                /* the shard's first population row */
+  const double *fitness;         /* [n] k_fitness' results */
+  const int32_t *frames;         /* [n, n_games] */
+  const int32_t *rows;           /* [n] or NULL */
+  const int32_t *n_active;       /* [1] device or NULL */
+  double *shard_fitness;         /* out [n] */
+  float *lineage;                /* in/out [row_lo + n] or NULL */
+} pg_scatter_args;
+int32_t pg_ga_scatter_fitness(const pg_scatter_args *args, void *stream);
+
+/* The generation's fitness: new_fitness[i] = invalid[i] ? fitness[i] :
+ * inherited[i] (varAnd's clones keep their parent's fitness; invalid NULL:
+ * every row evaluated), the logbook statistics of main.py:158-162 and the
+ * hall-of-fame candidates -- rows with new_fitness > worst (filter: a full
+ * hall admits only those, HallOfFame.update) or every row -- in ascending row
+ * order.  summary[8] = {any NaN (calculate_reward's ZeroDivisionError,
+ * utils.py:106-108), mean, std (ddof 0), min, max over the non-NaN values,
+ * nevals (rows evaluated), k (candidates), 0}; every reduction in a fixed
+ * order (reproducible).  new_fitness may alias fitness. */
+typedef struct pg_merge_args {
+  int32_t pop_n;
+  const double *fitness;         /* [pop_n] evaluated fitness (gathered over ranks) */
+  const uint8_t *invalid;        /* [pop_n] or NULL */
+  const double *inherited;       /* [pop_n] (read where invalid[i] == 0) */
+  double *new_fitness;           /* out [pop_n] */
+  int32_t filter;
+  double worst;
+  int32_t *cand;                 /* out [pop_n]: the first k entries */
+  double *cand_fitness;          /* out [pop_n] */
+  double *summary;               /* out [8] device */
+  void *workspace;               /* >= pg_ga_merge_workspace_bytes(pop_n) */
+  size_t workspace_bytes;
+} pg_merge_args;
+size_t pg_ga_merge_workspace_bytes(int32_t pop_n);
+int32_t pg_ga_merge_fitness(const pg_merge_args *args, void *stream);
+
+/* pg_ga_select_tournament_ranked with its stable fitness sort inside (one call). */
+size_t pg_ga_select_workspace_bytes(int32_t n_pop);
+int32_t pg_ga_select_ranked(const pg_select_args *args, void *workspace, size_t workspace_bytes, void *stream);
+
+/* What offspring slot i inherits from its parent chosen[i] (varAnd clones the
+ * chosen individuals): inherited[i] = fitness[chosen[i]] and lineage_out[i] =
+ * lineage_in[chosen[i]]; either output may be NULL. */
+int32_t pg_ga_inherit(const int32_t *chosen, int32_t n, const double *fitness, double *inherited,
+                      const float *lineage_in, float *lineage_out, void *stream);
+
+/* A shard's evaluation order (which rows toolbox.map(evaluate, invalid_ind)
+ * plays, main.py:165-170, and in what order): rows[0, *count) = the shard's
+ * invalid rows (invalid NULL: all), by_length: the longest lineage[row] first,
+ * ties by row; then the valid rows (clones) by row.  invalid and lineage are
+ * indexed by population row. */
+size_t pg_ga_order_workspace_bytes(int32_t n);
+int32_t pg_ga_order(int32_t n, int32_t row_lo, const uint8_t *invalid, const float *lineage, int32_t by_length,
+                    int32_t *rows, int32_t *count, void *workspace, size_t workspace_bytes, void *stream);
+
+/* HallOfFame.update's scan input for k known candidates (pg_ga_merge_fitness'
+ * cand list): their pg_row_hash values, and the packing of pg_hof_rank_classes
+ * -- ranks from a sort of the candidates alone plus binary searches into the
+ * members' items order, dense classes (a member's: the first member of equal
+ * hash; a candidate's: that member, else hof_n + the first candidate of equal
+ * hash) from two hash tables. */
+typedef struct pg_hof_cand_args {
+  int32_t hof_n;
+  const double *hof_fitness;     /* [hof_n] items order (descending) */
+  const uint64_t *hof_hash;      /* [hof_n] */
+  int32_t k;
+  const int32_t *cand;           /* [k] population rows, ascending */
+  const double *cand_fitness;    /* [k] */
+  const void *rows;              /* [*, stride] population rows, dtype */
+  int64_t stride;
+  int64_t genes;
+  int32_t dtype;
+  uint64_t *cand_hash;           /* out [k] */
+  int64_t *packed;               /* out [hof_n + 2k] */
+  void *workspace;               /* >= pg_hof_prepare_cand_workspace_bytes(hof_n, k) */
+  size_t workspace_bytes;
+} pg_hof_cand_args;
+size_t pg_hof_prepare_cand_workspace_bytes(int32_t hof_n, int32_t k);
+int32_t pg_hof_prepare_cand(const pg_hof_cand_args *args, void *stream);
+
+/* The new hall (HallOfFame.insert's deepcopy of each entrant): member j from
+ * pg_hof_update's new_src[j] = src[j]: old member src[j] < n_old (rows
+ * old_rows, hash old_hash) or candidate c = src[j] - n_old (population row
+ * cand[c], hash cand_hash[c]); new_fitness[j] = fitness_in[j].  Outputs
+ * disjoint from the inputs. */
+typedef struct pg_hof_commit_args {
+  void *dst;
+  int64_t dst_stride;
+  const void *old_rows;
+  int64_t old_stride;
+  const void *rows;
+  int64_t rows_stride;
+  const int32_t *cand;
+  const int32_t *src;            /* [m] device */
+  int32_t n_old;
+  int32_t m;
+  int64_t genes;
+  int32_t dtype;
+  const uint64_t *old_hash;
+  const uint64_t *cand_hash;
+  uint64_t *new_hash;            /* out [m] */
+  const double *fitness_in;      /* [m] device */
+  double *new_fitness;           /* out [m] */
+} pg_hof_commit_args;
+int32_t pg_hof_commit(const pg_hof_commit_args *args, void *stream);
+
 /* dst row j = old_rows[src[j]] if src[j] < n_old, else rows[index[src[j] - n_old]]
  * (index NULL: rows[src[j] - n_old]) -- pg_hof_update's new_src applied in one
  * pass; strides in elements, dst disjoint from both sources. */

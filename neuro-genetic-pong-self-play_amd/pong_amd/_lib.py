@@ -16,7 +16,7 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 4
+PG_ABI_VERSION = 5
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -124,6 +124,40 @@ class PgHofPrepareArgs(ctypes.Structure):
     ]
 
 
+class PgScatterArgs(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32), ("n_games", ctypes.c_int32), ("row_lo", ctypes.c_int32),
+        ("fitness", _vp), ("frames", _vp), ("rows", _vp), ("n_active", _vp), ("shard_fitness", _vp),
+        ("lineage", _vp),
+    ]
+
+
+class PgMergeArgs(ctypes.Structure):
+    _fields_ = [
+        ("pop_n", ctypes.c_int32), ("fitness", _vp), ("invalid", _vp), ("inherited", _vp), ("new_fitness", _vp),
+        ("filter", ctypes.c_int32), ("worst", ctypes.c_double), ("cand", _vp), ("cand_fitness", _vp),
+        ("summary", _vp), ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class PgHofCandArgs(ctypes.Structure):
+    _fields_ = [
+        ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("hof_hash", _vp), ("k", ctypes.c_int32),
+        ("cand", _vp), ("cand_fitness", _vp), ("rows", _vp), ("stride", ctypes.c_int64),
+        ("genes", ctypes.c_int64), ("dtype", ctypes.c_int32), ("cand_hash", _vp), ("packed", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class PgHofCommitArgs(ctypes.Structure):
+    _fields_ = [
+        ("dst", _vp), ("dst_stride", ctypes.c_int64), ("old_rows", _vp), ("old_stride", ctypes.c_int64),
+        ("rows", _vp), ("rows_stride", ctypes.c_int64), ("cand", _vp), ("src", _vp), ("n_old", ctypes.c_int32),
+        ("m", ctypes.c_int32), ("genes", ctypes.c_int64), ("dtype", ctypes.c_int32), ("old_hash", _vp),
+        ("cand_hash", _vp), ("new_hash", _vp), ("fitness_in", _vp), ("new_fitness", _vp),
+    ]
+
+
 # name -> (restype, argtypes); exactly the functions include/pong_ga.h declares
 SIGNATURES = {
     "pg_version": (ctypes.c_char_p, []),
@@ -150,6 +184,18 @@ SIGNATURES = {
     "pg_hof_prepare": (ctypes.c_int32, [ctypes.POINTER(PgHofPrepareArgs), _vp]),
     "pg_gather_rows": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp, _vp,
                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp]),
+    "pg_ga_scatter_fitness": (ctypes.c_int32, [ctypes.POINTER(PgScatterArgs), _vp]),
+    "pg_ga_merge_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "pg_ga_merge_fitness": (ctypes.c_int32, [ctypes.POINTER(PgMergeArgs), _vp]),
+    "pg_ga_select_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "pg_ga_select_ranked": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp, ctypes.c_size_t, _vp]),
+    "pg_ga_inherit": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "pg_ga_order_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "pg_ga_order": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp,
+                                     ctypes.c_size_t, _vp]),
+    "pg_hof_prepare_cand_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "pg_hof_prepare_cand": (ctypes.c_int32, [ctypes.POINTER(PgHofCandArgs), _vp]),
+    "pg_hof_commit": (ctypes.c_int32, [ctypes.POINTER(PgHofCommitArgs), _vp]),
     "pg_render_frames": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp]),
     "pg_find_stuff": (ctypes.c_int32, [_vp, ctypes.c_int64, ctypes.c_int32, _vp, _vp]),
 }

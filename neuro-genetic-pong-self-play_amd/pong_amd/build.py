@@ -10,7 +10,7 @@ from ._lib import LIB_PATH, PKG_DIR, REPO_DIR
 
 CSRC = os.path.join(PKG_DIR, "csrc")
 # one translation unit per kernel family, compiled in parallel and linked into one .so
-SOURCES = [os.path.join(CSRC, f) for f in ("pong_ga.hip", "pg_wide.hip", "pg_pixels.hip", "pg_staged.hip", "pg_service_more.hip", "pg_hof.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("pong_ga.hip", "pg_wide.hip", "pg_pixels.hip", "pg_staged.hip", "pg_service_more.hip", "pg_hof.hip", "pg_gen.hip")]
 DEPS = SOURCES + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp", "pg_cascade.hpp", "pg_service.hpp")] + [
     os.path.join(REPO_DIR, "include", "pong_ga.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -512,3 +512,153 @@ def find_stuff(frames: torch.Tensor) -> torch.Tensor:
         L.check("pg_find_stuff", L.lib().pg_find_stuff(_ptr(frames), frames[0].numel() if n else 100800, n, _ptr(out),
                                                        _stream(frames.device)))
     return out
+
+
+# ------------------------------------------------ one generation's device work
+class Workspaces:
+    """Grow-only device scratch buffers by name (the C-ABI keeps no allocations)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self._bufs = {}
+
+    def get(self, name: str, nbytes: int) -> torch.Tensor:
+        b = self._bufs.get(name)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+            self._bufs[name] = b
+        return b
+
+    def tensor(self, name: str, shape, dtype) -> torch.Tensor:
+        """A typed view of buffer ``name`` with at least ``shape`` elements."""
+        n = 1
+        for s in (shape if isinstance(shape, (tuple, list)) else (shape,)):
+            n *= int(s)
+        item = torch.empty((), dtype=dtype).element_size()
+        return self.get(name, n * item)[: n * item].view(dtype).view(shape)
+
+
+def scatter_fitness(res: EvalResult, n: int, row_lo: int, rows: Optional[torch.Tensor], count: Optional[torch.Tensor],
+                    shard_fitness: torch.Tensor, lineage: Optional[torch.Tensor]) -> torch.Tensor:
+    """pg_ga_scatter_fitness: the evaluation's fitness in shard row order (rows
+    not played read 0) and each played row's longest game into ``lineage``."""
+    dev = shard_fitness.device
+    _need(shard_fitness, "shard_fitness", torch.float64, dev, (n,))
+    if lineage is not None:
+        _need(lineage, "lineage", torch.float32, dev)
+    games = res.frames.shape[1] if res.frames.dim() == 2 else 1
+    a = L.PgScatterArgs(n, games, row_lo, _ptr(res.fitness), _ptr(res.frames), _ptr(rows), _ptr(count),
+                        _ptr(shard_fitness), _ptr(lineage))
+    with torch.cuda.device(dev):
+        L.check("pg_ga_scatter_fitness", L.lib().pg_ga_scatter_fitness(ctypes.byref(a), _stream(dev)))
+    return shard_fitness
+
+
+def merge_fitness(fitness: torch.Tensor, invalid: Optional[torch.Tensor], inherited: Optional[torch.Tensor],
+                  new_fitness: torch.Tensor, worst: Optional[float], cand: torch.Tensor, cand_fitness: torch.Tensor,
+                  summary: torch.Tensor, ws: Workspaces) -> None:
+    """pg_ga_merge_fitness (see pong_ga.h): new fitness, logbook summary, candidates."""
+    dev = fitness.device
+    n = fitness.shape[0]
+    _need(fitness, "fitness", torch.float64, dev, (n,))
+    _need(new_fitness, "new_fitness", torch.float64, dev, (n,))
+    _need(cand, "cand", torch.int32, dev, (n,))
+    _need(cand_fitness, "cand_fitness", torch.float64, dev, (n,))
+    _need(summary, "summary", torch.float64, dev, (8,))
+    if invalid is not None:
+        _need(invalid, "invalid", torch.uint8, dev, (n,))
+        _need(inherited, "inherited", torch.float64, dev, (n,))
+    nbytes = int(L.lib().pg_ga_merge_workspace_bytes(n))
+    w = ws.get("merge", nbytes)
+    a = L.PgMergeArgs(n, _ptr(fitness), _ptr(invalid), _ptr(inherited), _ptr(new_fitness),
+                      0 if worst is None else 1, 0.0 if worst is None else float(worst), _ptr(cand),
+                      _ptr(cand_fitness), _ptr(summary), _ptr(w), w.numel())
+    with torch.cuda.device(dev):
+        L.check("pg_ga_merge_fitness", L.lib().pg_ga_merge_fitness(ctypes.byref(a), _stream(dev)))
+
+
+def select_ranked(fitness: torch.Tensor, k: int, tournsize: int, seed: int, generation: int, ws: Workspaces,
+                  chosen: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """pg_ga_select_ranked: select_tournament_ranked with the sort inside, one call."""
+    dev = fitness.device
+    _need(fitness, "fitness", torch.float64, dev)
+    if chosen is None:
+        chosen = torch.empty(k, dtype=torch.int32, device=dev)
+    nbytes = int(L.lib().pg_ga_select_workspace_bytes(fitness.shape[0]))
+    w = ws.get("select", nbytes)
+    a = L.PgSelectArgs(fitness.shape[0], k, tournsize, _ptr(fitness), _ptr(chosen), seed, generation)
+    with torch.cuda.device(dev):
+        L.check("pg_ga_select_ranked", L.lib().pg_ga_select_ranked(ctypes.byref(a), _ptr(w), w.numel(), _stream(dev)))
+    return chosen
+
+
+def inherit(chosen: torch.Tensor, fitness: torch.Tensor, inherited: torch.Tensor, lineage_in: torch.Tensor,
+            lineage_out: torch.Tensor) -> None:
+    """pg_ga_inherit: inherited = fitness[chosen], lineage_out = lineage_in[chosen]."""
+    dev = chosen.device
+    n = chosen.shape[0]
+    _need(chosen, "chosen", torch.int32, dev, (n,))
+    _need(inherited, "inherited", torch.float64, dev, (n,))
+    _need(lineage_out, "lineage_out", torch.float32, dev, (n,))
+    with torch.cuda.device(dev):
+        L.check("pg_ga_inherit", L.lib().pg_ga_inherit(_ptr(chosen), n, _ptr(fitness), _ptr(inherited),
+                                                       _ptr(lineage_in), _ptr(lineage_out), _stream(dev)))
+
+
+def order(n: int, row_lo: int, invalid: Optional[torch.Tensor], lineage: Optional[torch.Tensor], by_length: bool,
+          rows: torch.Tensor, count: torch.Tensor, ws: Workspaces) -> None:
+    """pg_ga_order: the shard's evaluation order (invalid rows first, longest lineage first)."""
+    dev = rows.device
+    _need(rows, "rows", torch.int32, dev, (n,))
+    _need(count, "count", torch.int32, dev, (1,))
+    nbytes = int(L.lib().pg_ga_order_workspace_bytes(n))
+    w = ws.get("order", nbytes)
+    with torch.cuda.device(dev):
+        L.check("pg_ga_order", L.lib().pg_ga_order(n, row_lo, _ptr(invalid), _ptr(lineage), 1 if by_length else 0,
+                                                   _ptr(rows), _ptr(count), _ptr(w), w.numel(), _stream(dev)))
+
+
+def hof_prepare_cand(hof_fitness: torch.Tensor, hof_hash: torch.Tensor, cand: torch.Tensor,
+                     cand_fitness: torch.Tensor, rows: torch.Tensor, genes: int, cand_hash: torch.Tensor,
+                     packed: torch.Tensor, ws: Workspaces) -> None:
+    """pg_hof_prepare_cand: hashes of the k candidates and the scan's packed input."""
+    dev = cand.device
+    hn, k = hof_fitness.shape[0], cand.shape[0]
+    _need(hof_fitness, "hof_fitness", torch.float64, dev, (hn,))
+    _need(hof_hash, "hof_hash", torch.int64, dev, (hn,))
+    _need(cand, "cand", torch.int32, dev, (k,))
+    _need(cand_fitness, "cand_fitness", torch.float64, dev, (k,))
+    _need(cand_hash, "cand_hash", torch.int64, dev, (k,))
+    _need(packed, "packed", torch.int64, dev, (hn + 2 * k,))
+    if rows.dim() != 2 or rows.dtype not in DTYPES or rows.stride(1) != 1 or rows.device != dev:
+        raise ValueError("rows must be a row-major [n, G] f32/f64 tensor on the candidates' device")
+    nbytes = int(L.lib().pg_hof_prepare_cand_workspace_bytes(hn, k))
+    if nbytes == 0:
+        msg = L.lib().pg_last_error()
+        raise L.PongGAError("pg_hof_prepare_cand_workspace_bytes", -1, msg.decode() if msg else "")
+    w = ws.get("hof_cand", nbytes)
+    stride = rows.stride(0) if rows.shape[0] > 1 else rows.shape[1]
+    a = L.PgHofCandArgs(hn, _ptr(hof_fitness), _ptr(hof_hash), k, _ptr(cand), _ptr(cand_fitness), _ptr(rows), stride,
+                        int(genes), DTYPES[rows.dtype], _ptr(cand_hash), _ptr(packed), _ptr(w), w.numel())
+    with torch.cuda.device(dev):
+        L.check("pg_hof_prepare_cand", L.lib().pg_hof_prepare_cand(ctypes.byref(a), _stream(dev)))
+
+
+def hof_commit(dst: torch.Tensor, old_rows: torch.Tensor, rows: torch.Tensor, cand: torch.Tensor, src: torch.Tensor,
+               n_old: int, genes: int, old_hash: torch.Tensor, cand_hash: torch.Tensor, new_hash: torch.Tensor,
+               fitness_in: torch.Tensor, new_fitness: torch.Tensor) -> None:
+    """pg_hof_commit: the new members' rows, hashes and fitness in one pass."""
+    dev = dst.device
+    m = src.shape[0]
+    _need(src, "src", torch.int32, dev, (m,))
+    _need(fitness_in, "fitness_in", torch.float64, dev, (m,))
+    for name, t in (("dst", dst), ("old_rows", old_rows), ("rows", rows)):
+        if t.dim() != 2 or t.dtype != dst.dtype or t.device != dev or t.stride(1) != 1:
+            raise ValueError(f"{name} must be a row-major [n, G] tensor of dst's dtype on dst's device")
+    if m > dst.shape[0] or m > new_hash.shape[0] or m > new_fitness.shape[0]:
+        raise ValueError("more members than destination rows")
+    a = L.PgHofCommitArgs(_ptr(dst), dst.stride(0), _ptr(old_rows), old_rows.stride(0), _ptr(rows), rows.stride(0),
+                          _ptr(cand), _ptr(src), int(n_old), m, int(genes), DTYPES[dst.dtype], _ptr(old_hash),
+                          _ptr(cand_hash), _ptr(new_hash), _ptr(fitness_in), _ptr(new_fitness))
+    with torch.cuda.device(dev):
+        L.check("pg_hof_commit", L.lib().pg_hof_commit(ctypes.byref(a), _stream(dev)))

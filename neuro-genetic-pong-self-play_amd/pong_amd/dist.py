@@ -23,7 +23,9 @@ def shard_range(n: int, rank: int, world: int):
 
 
 def gather_fitness(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
-    """All-gather each rank's fitness shard into the full [n_total] vector, in row order."""
+    """All-gather each rank's fitness shard into the full [n_total] vector, in
+    row order (a [rows, c] shard: the full [n_total, c] table, e.g. fitness
+    beside each row's longest game)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     lo, hi = shard_range(n_total, rank, world)
@@ -34,9 +36,10 @@ def gather_fitness(local: torch.Tensor, n_total: int, group=None) -> torch.Tenso
     # host tensors; RCCL ("nccl") gathers device memory over xGMI directly
     stage = local.is_cuda and dist.get_backend(group) == "gloo"
     dev = torch.device("cpu") if stage else local.device
-    buf = torch.zeros(width, dtype=local.dtype, device=dev)
+    tail = tuple(local.shape[1:])
+    buf = torch.zeros((width,) + tail, dtype=local.dtype, device=dev)
     buf[: hi - lo] = local.to(dev)
-    out = torch.empty(width * world, dtype=local.dtype, device=dev)
+    out = torch.empty((width * world,) + tail, dtype=local.dtype, device=dev)
     if stage:
         dist.all_gather(list(out.split(width)), buf, group=group)
     else:

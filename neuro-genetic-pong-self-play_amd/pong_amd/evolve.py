@@ -99,6 +99,16 @@ class DeviceGA:
         # candidates, hashes, ranks, classes); False: the same scan input from
         # torch ops (nonzero, stable sort, unique), kept as the cross-check
         self.native_prepare = True
+        # the generation's device work around the evaluation in few native
+        # launches and two host syncs (csrc/pg_gen.hip): False runs the torch
+        # formulation above (the cross-check of tests/test_gpu_generation.py)
+        self.fused = True
+        self.ws = D.Workspaces(self.device)
+        self._lineage_alt = torch.zeros_like(self.lineage_frames)
+        self._hof_hash_alt = torch.zeros_like(self.hof_hash)
+        self._hof_fitness_alt = torch.zeros_like(self.hof_fitness)
+        self._fit_alt = torch.zeros_like(self.fitness)
+        self._summary_h = torch.zeros(8, dtype=torch.float64, pin_memory=True)
 
     # ------------------------------------------------------------ views
     @property
@@ -342,6 +352,9 @@ class DeviceGA:
 
     def step(self) -> dict:
         """One eaSimple generation (or, first, the initial evaluation); returns the logbook row."""
+        return self._step_fused() if self.fused else self._step_torch()
+
+    def _step_torch(self) -> dict:
         if self.generation < 0:
             fit = self._evaluate(0, self.population, ~self.valid)
             nevals = int((~self.valid).sum())
@@ -371,6 +384,172 @@ class DeviceGA:
         # store[H:] (this generation's parents, free now), the buffer the swap
         # below makes next step's spare[H:]
         self._hof_update(new_fit, off, self.spare, overlap=lambda: self._prefetch(g + 1, off, new_fit, self.store))
+        self._mark("hall_of_fame")
+        self.fitness = new_fit
+        self.store, self.spare = self.spare, self.store
+        self.generation = g
+        rec = self._record(g, nevals, stats)
+        self._mark("record")
+        return rec
+
+    # ------------------------------------------------- fused generation path
+    # One generation = [prefetched: select, vary, inherit, order] -> schedule +
+    # evaluation -> scatter (+ all-gather) -> merge (new fitness, statistics,
+    # candidates) -> sync 1 -> candidates' hashes, ranks, classes -> sync 2,
+    # with the next generation's select/vary/inherit/order enqueued meanwhile
+    # -> host scan -> one upload -> commit.  Same semantics as _step_torch
+    # (population, fitness, hall of fame equal; the statistics' last bits may
+    # differ: they are reduced in a fixed order of their own).
+    def _buf(self, name, shape, dtype):
+        return self.ws.tensor(name, shape, dtype)
+
+    def _next_gen_prep(self, g: int, parents: torch.Tensor, fitness: torch.Tensor, store: torch.Tensor):
+        """Generation g's selTournament + varAnd into store[H:], what the clones
+        inherit, and the shard's evaluation order; kept in self._next."""
+        chosen = self._buf("chosen", self.P, torch.int32)
+        D.select_ranked(fitness, self.P, self.tournsize, self.seed, g, self.ws, chosen=chosen)
+        _, inv = D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu, self.sigma, self.indpb,
+                        seed=self.seed, generation=g, out=store[self.H:])
+        inherited = self._buf("inherited", self.P, torch.float64)
+        D.inherit(chosen, fitness, inherited, self.lineage_frames, self._lineage_alt)
+        self.lineage_frames, self._lineage_alt = self._lineage_alt, self.lineage_frames
+        self._next = (g, inv, inherited, self._order(inv, g))
+
+    def _order(self, inv_u8: Optional[torch.Tensor], g: int = 0):
+        # by generation parity: generation g + 1's order is made while
+        # generation g's (self.last_rows / last_count) is still read
+        n = self.hi - self.lo
+        local = self._buf("local_rows%d" % (g & 1), n, torch.int32)
+        count = self._buf("local_count%d" % (g & 1), 1, torch.int32)
+        D.order(n, self.lo, inv_u8, self.lineage_frames, self.order_by_length, local, count, self.ws)
+        return local, count
+
+    def _evaluate_fused(self, g: int, rows: torch.Tensor, order) -> torch.Tensor:
+        lo, hi = self.lo, self.hi
+        n = hi - lo
+        local, count = order
+        kind, opp, mult = D.schedule(self.schedule, n, self.n_games, lo, self.hof_fitness, self.hof_n,
+                                     self.seed, g, self.device, rows=local)
+        opponents = self.store[: self.hof_n] if self.hof_n else None
+        out = self.last if (self.last is not None and self.last.fitness.shape[0] == n) else None
+        if self.eval_events is not None:
+            self.eval_events[0].record()
+        res, _ = self.ev.evaluate(rows, kind, opp, mult, opponents=opponents, out=out, validate=False,
+                                  hard_log=self.hard_log, rows=local, n_active=count)
+        if self.eval_events is not None:
+            self.eval_events[1].record()
+        self.last, self.last_rows, self.last_count = res, local, count
+        if self.on_evaluate is not None:
+            self.on_evaluate(g, rows, opponents, res)
+        shard = self._buf("shard_fit", n, torch.float64)
+        D.scatter_fitness(res, n, lo, local, count, shard, self.lineage_frames)
+        if not dist.is_initialized():
+            return shard
+        # the fitness all-gather also carries each row's longest game, so every
+        # rank orders its next shard from the same predictions
+        both = torch.stack([shard, self.lineage_frames[lo:hi].double()], dim=1)
+        full = PD.gather_fitness(both, self.P, self.group)
+        self.lineage_frames.copy_(full[:, 1].float())
+        return full[:, 0].contiguous()
+
+    def _merge(self, fit: torch.Tensor, inv: Optional[torch.Tensor], inherited: Optional[torch.Tensor],
+               worst: Optional[float]):
+        """pg_ga_merge_fitness + the generation's first sync: (new fitness,
+        candidates, their fitness, stats, nevals, k)."""
+        new_fit = self._fit_alt
+        cand = self._buf("cand", self.P, torch.int32)
+        cand_fit = self._buf("cand_fit", self.P, torch.float64)
+        summ = self._buf("summary", 8, torch.float64)
+        D.merge_fitness(fit, inv, inherited, new_fit, worst, cand, cand_fit, summ, self.ws)
+        self._summary_h.copy_(summ, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        ev.synchronize()
+        v = self._summary_h.tolist()
+        if v[0]:
+            # a NaN fitness is a game whose calculate_reward divided by zero (utils.py:106-108)
+            raise ZeroDivisionError("float division by zero (calculate_reward with total_frames == 0)")
+        self._fit_alt = self.fitness
+        return new_fit, cand, cand_fit, v[1:5], int(v[5]), int(v[6])
+
+    def _hof_update_fused(self, rows: torch.Tensor, cand: torch.Tensor, cand_fit: torch.Tensor, k: int,
+                          dst: torch.Tensor, overlap=None):
+        """HallOfFame.update over the k candidates (rows ``rows[cand]``); the
+        members are written to dst[:new_n] (disjoint from the current members and rows)."""
+        if self.H == 0:
+            if overlap:
+                overlap()
+            return
+        old_n = self.hof_n
+        if k == 0:
+            dst[:old_n] = self.store[:old_n]
+            if overlap:
+                overlap()
+            return
+        if self.profile is not None:
+            self.profile["hof_candidates"] = self.profile.get("hof_candidates", 0) + k
+        n = old_n + k
+        cand, cand_fit = cand[:k], cand_fit[:k]
+        cand_hash = self._buf("cand_hash", k, torch.int64)
+        packed = self._buf("packed", n + k, torch.int64)
+        D.hof_prepare_cand(self.hof_fitness[:old_n], self.hof_hash[:old_n], cand, cand_fit, rows, self.G, cand_hash,
+                           packed, self.ws)
+        packed_h = torch.empty(n + k, dtype=torch.int64, pin_memory=True)
+        packed_h.copy_(packed, non_blocking=True)
+        copied = torch.cuda.Event()
+        copied.record()
+        if overlap:
+            overlap()
+        copied.synchronize()
+        pk = packed_h.numpy()
+        self._mark("hof_prepare", sub=True)
+        rank_np = (pk[:n] & 0xFFFFFFFF).astype(np.int32)
+        cls_np = pk[:n] >> 32
+        src, new_fit = D.hof_update(self.H, self._hof_fit_host, cls_np[:old_n], pk[n:].view(np.float64),
+                                    cls_np[old_n:], rank=rank_np)
+        self._mark("hof_scan", sub=True)
+        m = src.shape[0]
+        up = torch.empty(3 * m, dtype=torch.int32, pin_memory=True)
+        upn = up.numpy()
+        upn[: 2 * m].view(np.float64)[:] = new_fit
+        upn[2 * m:] = src
+        up_d = up.to(self.device, non_blocking=True)
+        D.hof_commit(dst, self.store, rows, cand, up_d[2 * m:], old_n, self.G, self.hof_hash, cand_hash,
+                     self._hof_hash_alt, up_d[: 2 * m].view(torch.float64), self._hof_fitness_alt)
+        self.hof_hash, self._hof_hash_alt = self._hof_hash_alt, self.hof_hash
+        self.hof_fitness, self._hof_fitness_alt = self._hof_fitness_alt, self.hof_fitness
+        self.hof_n = int(m)
+        self._hof_fit_host = new_fit
+
+    def _step_fused(self) -> dict:
+        worst = float(self._hof_fit_host[-1]) if (self.H and self.hof_n >= self.H) else None
+        if self.generation < 0:
+            inv = (~self.valid).to(torch.uint8)
+            fit = self._evaluate_fused(0, self.population, self._order(inv))
+            new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, self.fitness, worst)
+            self.fitness, self.valid = new_fit, torch.ones_like(self.valid)
+            # generation 1's offspring go to spare[H:] (no swap after the initial update)
+            self._hof_update_fused(self.population, cand, cand_fit, k, self.spare,
+                                   overlap=lambda: self._next_gen_prep(1, self.population, new_fit, self.spare))
+            self.store[: self.hof_n] = self.spare[: self.hof_n]
+            self.generation = 0
+            return self._record(0, nevals, stats)
+        g = self.generation + 1
+        self._mark(None)
+        off = self.spare[self.H:]
+        if self._next is None or self._next[0] != g:
+            self._next_gen_prep(g, self.population, self.fitness, self.spare)
+        _, inv, inherited, order = self._next
+        self._next = None
+        self._mark("select_vary")
+        fit = self._evaluate_fused(g, off, order)  # invalid_ind only: clones keep their parent's fitness
+        new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, inherited, worst)
+        self._mark("evaluate")
+        # generation g + 1's parents are this offspring; its offspring go to
+        # store[H:] (this generation's parents, free now), the buffer the swap
+        # below makes next step's spare[H:]
+        self._hof_update_fused(off, cand, cand_fit, k, self.spare,
+                               overlap=lambda: self._next_gen_prep(g + 1, off, new_fit, self.store))
         self._mark("hall_of_fame")
         self.fitness = new_fit
         self.store, self.spare = self.spare, self.store
