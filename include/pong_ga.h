@@ -139,14 +139,15 @@ typedef struct pg_eval_args {
   int32_t *frames;               /* [n_genomes, n_games] env.step calls */
   double *total_frames;          /* [n_genomes, n_games] main.py:73 accumulator */
   int32_t *status;               /* [n_genomes] 1 = ZeroDivisionError in calculate_reward */
-  uint64_t *counters;            /* optional [12]: [0] env steps simulated, [1] NN forwards,
-                                    [2] numpy-order f64 forwards, [3] games; split kernel: [4] f32
-                                    certificate failures, [5] failures decided by the service wave's
+  uint64_t *counters;            /* optional [16]: [0] env steps stepped one frame at a time, [1] NN
+                                    forwards, [2] numpy-order f64 forwards, [3] games; split kernel: [4]
+                                    f32 certificate failures, [5] failures decided by the service wave's
                                     certified f64 rules, [6] failures decided in-wave by the f32 plateau
                                     rule; wide kernel: [7] network weight passes; split and wide
-                                    kernels: [8] episode frames not simulated because the rally was
-                                    periodic (frames = [0] + [8]); [9] hard decisions (see hard_log);
-                                    [10..11] 0 */
+                                    kernels: [8] episode frames of periodic rallies advanced to their
+                                    timeout at once; [9] hard decisions (see hard_log); split kernel:
+                                    [12] serve-delay frames advanced at once (ball hidden); the
+                                    episodes' frames = [0] + [8] + [12]; [10], [11], [13..15] 0 */
   uint8_t *trace;                /* optional [trace_games, trace_cap] per-frame action codes */
   int32_t trace_games;           /* games (genome-major index g = i*n_games + game) traced */
   int32_t trace_cap;

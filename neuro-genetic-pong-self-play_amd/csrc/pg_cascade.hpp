@@ -246,6 +246,72 @@ __device__ __forceinline__ void load_net_pk(NetP<U, O> &n, const WT *__restrict_
   n.e = group_sum<L>(weights_ok(big) ? 0.f : 1.f) > 0.f ? __builtin_inff() : e;
 }
 
+// ---- lane records: what load_net_pk leaves in one lane's registers, laid
+// out flat (w1 pairs, w2 pairs, c, e; padded to whole 16-B pieces) so a game
+// start is rec_floats / 4 independent 16-B loads and one wait instead of the
+// genome gather, the f32 conversion, the x-flip fold and the bound's group
+// sums (k_prep_records prepares every network of a launch once).
+template <int U, int O>
+__host__ __device__ constexpr int rec_floats() {
+  return ((U + 1) / 2 * 2 * (7 + O) + O + 1 + 3) / 4 * 4;
+}
+
+template <int U, int O>
+__device__ __forceinline__ void store_rec(const NetP<U, O> &n, float *__restrict__ r) {
+  constexpr int P = NetP<U, O>::P;
+  constexpr int F = rec_floats<U, O>();
+  float v[F];
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      v[(p * 7 + i) * 2] = n.w1[p][i].x;
+      v[(p * 7 + i) * 2 + 1] = n.w1[p][i].y;
+    }
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      v[P * 14 + (p * O + o) * 2] = n.w2[p][o].x;
+      v[P * 14 + (p * O + o) * 2 + 1] = n.w2[p][o].y;
+    }
+#pragma unroll
+  for (int o = 0; o < O; ++o) v[P * 14 + P * O * 2 + o] = n.c[o];
+  v[P * 14 + P * O * 2 + O] = n.e;
+#pragma unroll
+  for (int f = P * 14 + P * O * 2 + O + 1; f < F; ++f) v[f] = 0.f;
+  float4 *d = reinterpret_cast<float4 *>(r);
+#pragma unroll
+  for (int q = 0; q < F / 4; ++q) d[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+template <int U, int O>
+__device__ __forceinline__ void load_rec(NetP<U, O> &n, const float *__restrict__ r) {
+  constexpr int P = NetP<U, O>::P;
+  constexpr int F = rec_floats<U, O>();
+  const float4 *s = reinterpret_cast<const float4 *>(r);
+  float v[F];
+#pragma unroll
+  for (int q = 0; q < F / 4; ++q) {
+    const float4 x = s[q];
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int i = 0; i < 7; ++i) n.w1[p][i] = float2v{v[(p * 7 + i) * 2], v[(p * 7 + i) * 2 + 1]};
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int o = 0; o < O; ++o) n.w2[p][o] = float2v{v[P * 14 + (p * O + o) * 2], v[P * 14 + (p * O + o) * 2 + 1]};
+#pragma unroll
+  for (int o = 0; o < O; ++o) n.c[o] = v[P * 14 + P * O * 2 + o];
+  n.e = v[P * 14 + P * O * 2 + O];
+}
+
 // Hidden layer and the lane-partial output sums of one packed network; k are
 // the six doubled-centroid features (x_i = k_i / 320 is folded into W1).
 template <int U, int O>

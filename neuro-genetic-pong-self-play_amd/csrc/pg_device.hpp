@@ -130,6 +130,17 @@ struct Pong {
     }
   }
 
+  // Top row of a paddle after h frames of clamp-only actions: with the ball
+  // hidden get_actions returns [0,0] (main.py:151-153) and
+  // keep_within_game_bounds_please (utils.py:71-77) moves a paddle whose
+  // centroid is < 16 down and > 144 up -- rows <= 8 down, rows >= 137 up, 3 px
+  // a frame (move() never clamps there) -- until it is inside [9, 136].
+  __device__ static int drift(int py, int h) {
+    const int down = py <= 8 ? min((11 - py) / 3, h) : 0;   // ceil((9 - py) / 3) frames
+    const int up = py >= 137 ? min((py - 134) / 3, h) : 0;  // ceil((py - 136) / 3) frames
+    return py + kPaddleSpeed * (down - up);
+  }
+
   __device__ void serve() {
     const uint64_t r = splitmix64(seed ^ ((uint64_t)(point + 1) * 0xD1B54A32D192ED03ull));
     const int sel = (int)((r >> 32) & 3u);

@@ -46,6 +46,7 @@ struct EvalParams {
   int trace_games, trace_cap;
   int nodes[PG_MAX_NODES];
   int n_nodes, bias, max_width;
+  float *recs;         // split kernel: lane records (k_prep_records), [n_genomes + n_opponents][L/2][rec_floats]
   void *wide_scratch;  // k_wide: the blocks' tile-major W2 copies (workspace)
   int wide_w3_resident;  // k_wide: every network's W3 kept in LDS for the genome's games
 };

@@ -18,6 +18,34 @@
 
 namespace pg {
 
+// Every network a launch plays, once, in the layout a game lane holds it
+// (load_net_pk: pre-scaled f32 weights, the left paddle's x-flip folded in,
+// the certificate's bound): record r < n_genomes is entry r's genome as the
+// right paddle, record n_genomes + j opponent row j as the left paddle.  HL
+// consecutive threads prepare one network (the bound's group sums).
+template <int L, int U, int O, typename WT>
+__global__ __launch_bounds__(256) void k_prep_records(EvalParams p) {
+  constexpr int HL = L / 2;
+  constexpr int F = rec_floats<U, O>();
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long net = t / HL;
+  const int hl = (int)(t % HL);
+  if (net >= (long)p.n_genomes + p.n_opponents) return;  // whole groups (HL divides 64)
+  const WT *g;
+  int flip;
+  if (net < p.n_genomes) {
+    if (net >= active_genomes(p)) return;  // not played by this launch
+    g = (const WT *)p.genomes + (long)genome_row(p, (int)net) * p.gstride;
+    flip = 0;
+  } else {
+    g = (const WT *)p.opponents + (net - p.n_genomes) * p.ostride;
+    flip = 1;
+  }
+  NetP<U, O> n;
+  load_net_pk<HL, U, O, WT>(n, g, p.nodes[1], p.bias, hl, flip);
+  store_rec<U, O>(n, p.recs + (net * HL + hl) * F);
+}
+
 template <int L, int U, int O, typename WT>
 __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   constexpr int kSvcThreads = svc_threads<U>();
@@ -100,7 +128,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   Pong st;
   int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
   const WT *gm = genomes;
-  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0;
+  uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0, hidden = 0;
 
   const int games_total = active_total(p);
   int w;
@@ -110,18 +138,31 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     w = group_broadcast<L>(ww, leader);
   }
   bool fresh = true;
+#ifdef PG_START_PROBE  // diagnostic build: shader cycles of the game-start blocks vs the wave's total
+  uint64_t probe_fresh = 0;
+  const uint64_t probe_t0 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef PG_TIMELINE
   uint64_t t_start = 0;
   uint32_t g_fails = 0, g_slow = 0;
 #endif
   while (w < games_total) {
+#ifdef PG_START_PROBE
+    const bool any_fresh = __builtin_amdgcn_ballot_w64(fresh) != 0;
+    const uint64_t probe_f0 = __builtin_amdgcn_s_memtime();
+#endif
     if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
       const int i = w / p.n_games;
       const int g = w - i * p.n_games;
       kind = p.kind[w];
       const WT *gr = genomes + (long)genome_row(p, i) * p.gstride;
-      gm = (side && kind == kOppNN) ? opponents + (long)p.opp[w] * p.ostride : gr;
-      load_net_pk<HL, U, O, WT>(net, gm, H, b, hl, side);  // the left network with the x-flip folded in
+      // the left half: opponent row opp (its record has the x-flip folded in);
+      // idle (a copy of the genome) against a scripted opponent.  A network
+      // game needs opponents (pong_ga.h); without any, the genome plays itself.
+      const bool nn = side && kind == kOppNN && p.n_opponents > 0;
+      const int oj = nn ? min(max(p.opp[w], 0), p.n_opponents - 1) : 0;
+      gm = nn ? opponents + (long)oj * p.ostride : gr;
+      load_rec<U, O>(net, p.recs + ((nn ? (long)p.n_genomes + oj : (long)i) * HL + hl) * rec_floats<U, O>());
       st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
       act_r = act_l = timeout = total = frames = 0;
       fresh = false;
@@ -131,6 +172,36 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       g_fails = g_slow = 0;
 #endif
     }
+#ifdef PG_START_PROBE
+    if (any_fresh) probe_fresh += __builtin_amdgcn_s_memtime() - probe_f0;
+#endif
+#ifndef PG_NO_HIDDEN_JUMP
+    // The serve delay in closed form: while the ball is hidden no point can be
+    // scored, nothing is decided by a network (get_actions: [0,0],
+    // main.py:151-153) and a paddle only drifts back inside the clamp band
+    // (Pong::drift), so the frames before the serve frame are advanced at
+    // once -- the same state, actions, timeout and frame counts as stepping
+    // them (never while tracing, which records every frame).
+    {
+#ifdef PG_TIMELINE
+      constexpr bool kTrace = false;
+#else
+      const bool kTrace = p.trace != nullptr;
+#endif
+      const bool hid = !kTrace && !st.vis && st.timer >= 2;
+      if (__builtin_amdgcn_ballot_w64(hid) != 0 && hid) {
+        const int h = st.timer - 1;
+        st.rpy = Pong::drift(st.rpy, h);
+        if (!st.one_player) st.lpy = Pong::drift(st.lpy, h);
+        st.timer = 1;
+        act_r = clamp_action(paddle_c2(st.rpy), 0);
+        act_l = clamp_action(paddle_c2(st.lpy), 0);
+        timeout += frames > 0 ? h : h - 1;  // frame 1 of a game does not count (main.py:94-96)
+        frames += h;
+        hidden += h;
+      }
+    }
+#endif
     const int s1b = st.s1, s2b = st.s2;
     const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
     st.step(act_r, act_l);
@@ -287,8 +358,10 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   }
   if (p.counters && c_games) {
     if (lig == 0) {
-      // env steps simulated: the episodes' frames minus those a periodic rally skipped
-      atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)(c_steps - skipped));
+      // env steps stepped one at a time: the episodes' frames minus those a
+      // periodic rally skipped [8] and the serve delays advanced at once [12]
+      atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)(c_steps - skipped - hidden));
+      if (hidden) atomicAdd((unsigned long long *)&p.counters[12], (unsigned long long)hidden);
       atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
       atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
       if (skipped) atomicAdd((unsigned long long *)&p.counters[8], (unsigned long long)skipped);
@@ -298,8 +371,21 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     if (hl == 0 && plateau) atomicAdd((unsigned long long *)&p.counters[5], (unsigned long long)plateau);
     if (hl == 0 && inwave) atomicAdd((unsigned long long *)&p.counters[6], (unsigned long long)inwave);
   }
+#ifdef PG_START_PROBE
+  if (p.counters && lane64 == 0) {
+    atomicAdd((unsigned long long *)&p.counters[13], (unsigned long long)probe_fresh);
+    atomicAdd((unsigned long long *)&p.counters[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - probe_t0));
+    atomicAdd((unsigned long long *)&p.counters[15], 1ull);
+  }
+#endif
   // this wave will post no more requests
   if (lane64 == 0) atomicAdd(&waves_done, 1);
+}
+
+// bytes of lane records a split launch needs (pg_eval_workspace_bytes)
+inline size_t service_records_bytes(int n_genomes, int n_opponents, int L, int U, int O) {
+  const int F = ((U + 1) / 2 * 2 * (7 + O) + O + 1 + 3) / 4 * 4;  // rec_floats<U, O>()
+  return ((size_t)n_genomes + (size_t)(n_opponents > 0 ? n_opponents : 0)) * (size_t)(L / 2) * F * sizeof(float);
 }
 
 template <int L, int U, int O, typename WT>
@@ -311,6 +397,9 @@ inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
   const int cap = num_cus() * 2;
   const int grid = want < cap ? want : cap;
   if (grid <= 0) return PG_OK;
+  if (!p.recs) return fail(PG_ERR_INVALID, "split kernel: no lane-record workspace");
+  const long prep_threads = ((long)p.n_genomes + p.n_opponents) * (L / 2);
+  hipLaunchKernelGGL((k_prep_records<L, U, O, WT>), dim3((unsigned)((prep_threads + 255) / 256)), dim3(256), 0, s, p);
   hipLaunchKernelGGL((k_service<L, U, O, WT>), dim3(grid), dim3(kSvcThreads), lds, s, p);
   PG_HIP(hipGetLastError());
   return PG_OK;
@@ -318,5 +407,15 @@ inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
 
 // layouts L != 8 or U != 16 (pg_service_more.hip); PG_ERR_UNSUPPORTED when none fits
 int32_t launch_service_more(const EvalParams &p, int L, int O, bool f64, hipStream_t s);
+
+// the units per lane the split dispatch instantiates for (L, H): launch_service_any
+// (pong_ga.hip: L = 8 with H in (32, 64] -> 16) and launch_more (pg_service_more.hip:
+// the smallest of 1, 2, 4, 8 with (L / 2) U >= H); 0 when none fits
+inline int service_units(int L, int H) {
+  if (L == 8 && H > 32 && H <= 64) return 16;
+  for (int u = 1; u <= 8; u *= 2)
+    if ((L / 2) * u >= H) return u;
+  return 0;
+}
 
 }  // namespace pg

@@ -789,11 +789,9 @@ static int32_t launch_service_any(const EvalParams &p, int L, int O, hipStream_t
 #else
   const bool here = L == 8 && H > 32 && H <= 64;
 #endif
-  if (here) {
-    if (O == 2) return launch_service<8, 16, 2, WT>(p, s);
-    if (O == 3) return launch_service<8, 16, 3, WT>(p, s);
-    if (O == 4) return launch_service<8, 16, 4, WT>(p, s);
-  }
+  // (only O = 3 here: the iterative scheduler's register allocator crashes
+  // ROCm 7.2's compiler on the O = 2 / 4 instances, built in pg_service_more.hip)
+  if (here && O == 3) return launch_service<8, 16, 3, WT>(p, s);
 #ifdef PG_DEV_MIN  // variant builds for experiments (tools/build_variant.sh): the bench layout only
   return fail(PG_ERR_UNSUPPORTED, "no service kernel for L=%d H=%d O=%d", L, H, O);
 #else
@@ -889,10 +887,22 @@ static int resolve_kernel(const pg_eval_args *a) {
   return PG_KERNEL_GENERAL;
 }
 
+// the split kernel's lane records (k_prep_records), after the base workspace
+static size_t split_records_bytes(const pg_eval_args *a) {
+  if (!resident_shape_ok(a->net) || a->n_genomes <= 0) return 0;
+  const int H = a->net.nodes[1];
+  const int L = a->group_lanes > 0 ? a->group_lanes : choose_split_lanes(H);
+  const int U = (L == 8 && H <= 64) ? 16 : service_units(L, H);  // >= what any build instantiates
+  if (U <= 0) return 0;
+  return (service_records_bytes(a->n_genomes, a->opponents ? a->n_opponents : 0, L, U, a->net.nodes[2]) + 255) /
+         256 * 256;
+}
+
 size_t pg_eval_workspace_bytes(const pg_eval_args *a) {
   size_t n = eval_base_workspace(a);
   if (!a) return n;
   const int kernel = resolve_kernel(a);
+  if (kernel == PG_KERNEL_SPLIT) n += split_records_bytes(a);
   if (kernel == PG_KERNEL_STAGED) n += (staged_workspace_bytes(a) + 255) / 256 * 256;
   if (kernel == PG_KERNEL_WIDE && wide_shape_ok(a->net, a->n_games)) n += (wide_workspace_bytes(a) + 255) / 256 * 256;
   return n;
@@ -978,6 +988,7 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "split kernel is the certified-precision path");
     const int H = a->net.nodes[1];
     const int L = a->group_lanes > 0 ? a->group_lanes : choose_split_lanes(H);
+    p.recs = (float *)((char *)a->workspace + eval_base_workspace(a));
     rc = a->net.dtype == PG_F64 ? launch_service_any<double>(p, L, a->net.nodes[2], s)
                                 : launch_service_any<float>(p, L, a->net.nodes[2], s);
     if (rc != PG_OK) return rc;

@@ -55,10 +55,11 @@ class EvalResult:
     frames: torch.Tensor        # [n, games] int32 env steps
     total_frames: torch.Tensor  # [n, games] f64
     status: torch.Tensor        # [n] int32, 1 = ZeroDivisionError
-    counters: torch.Tensor      # [12] int64 (pg_eval_args.counters): [0] env steps simulated, [1] NN
-    #                             forwards, [2] numpy-order f64 forwards, [3] games, [4..6] certificate
-    #                             cascade (split), [7] network passes (wide), [8] frames of periodic
-    #                             rallies not simulated (the episodes' frames = [0] + [8])
+    counters: torch.Tensor      # [16] int64 (pg_eval_args.counters): [0] env steps stepped one frame at
+    #                             a time, [1] NN forwards, [2] numpy-order f64 forwards, [3] games,
+    #                             [4..6] certificate cascade (split), [7] network passes (wide), [8]
+    #                             frames of periodic rallies advanced at once, [12] serve-delay frames
+    #                             advanced at once (the episodes' frames = [0] + [8] + [12])
 
 
 class Evaluator:
@@ -152,7 +153,7 @@ class Evaluator:
                 frames=torch.empty((n, games), dtype=torch.int32, device=dev),
                 total_frames=torch.empty((n, games), dtype=torch.float64, device=dev),
                 status=torch.empty(n, dtype=torch.int32, device=dev),
-                counters=torch.zeros(12, dtype=torch.int64, device=dev))
+                counters=torch.zeros(16, dtype=torch.int64, device=dev))
         else:
             out.counters.zero_()
         trace = None

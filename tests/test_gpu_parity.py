@@ -162,7 +162,7 @@ def test_eval_matches_oracle(gpu, oracle, shape, dist):
     res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
     _assert_same(res, ref)
     # simulated env steps + periodic-rally frames not simulated = the episodes' frames
-    assert int(res.counters[0]) + int(res.counters[8]) == int(ref["frames"].sum())
+    assert int(res.counters[0]) + int(res.counters[8]) + int(res.counters[12]) == int(ref["frames"].sum())
     if len(shape) == 3:  # the other kernels must agree too
         for kernel, precision in (("general", "f64"), ("resident", "certified")):
             res2, _ = ev.evaluate(_dev_genomes(genomes, gpu), torch.tensor(kinds, device=gpu),
@@ -317,7 +317,7 @@ def test_full_size_properties(gpu, oracle):
     r3, _ = ev.evaluate(genomes[perm].contiguous(), kind[perm].contiguous(), opp[perm].contiguous(),
                         mult[perm].contiguous(), opponents=opponents)
     assert torch.equal(r3.fitness, f1[perm])
-    assert int(r1.counters[3]) == n * 6 and int(r1.counters[0]) + int(r1.counters[8]) == int(r1.frames.sum())
+    assert int(r1.counters[3]) == n * 6 and int(r1.counters[0]) + int(r1.counters[8]) + int(r1.counters[12]) == int(r1.frames.sum())
     assert int(r1.counters[8]) > 0  # periodic rallies were jumped to their timeout
     sc = r1.scores.cpu().numpy()
     assert sc.max() <= 3 and sc.min() >= 0

@@ -31,7 +31,7 @@ def test_staged_matches_oracle(gpu, oracle, shape, dist):
     res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
     _assert_same(res, ref)
     c = res.counters.cpu().numpy()
-    assert int(c[0]) + int(c[8]) == int(ref["frames"].sum())
+    assert int(c[0]) + int(c[8]) + int(c[12]) == int(ref["frames"].sum())
     assert int(c[3]) == n * 6
 
 

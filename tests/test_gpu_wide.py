@@ -68,7 +68,7 @@ def test_wide_matches_oracle(gpu, oracle, shape, bias, dt):
     res, _ = _eval(ev, gpu, genomes, opponents, kinds, opp, mult)
     ref = oracle.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents, bias=bias, n_threads=8)
     _same(res, ref)
-    assert int(res.counters[0]) + int(res.counters[8]) == int(ref["frames"].sum())
+    assert int(res.counters[0]) + int(res.counters[8]) + int(res.counters[12]) == int(ref["frames"].sum())
     assert int(res.counters[3]) == n * 6
 
 
@@ -131,7 +131,7 @@ def test_wide_selfplay_properties(gpu):
     r2, _ = ev.evaluate(genomes[perm].contiguous(), kind[perm].contiguous(), opp[perm].contiguous(),
                         mult[perm].contiguous(), opponents=opponents)
     assert torch.equal(r2.fitness, f1[perm]) and torch.equal(r2.frames, r1.frames[perm])
-    assert int(r1.counters[3]) == n * 6 and int(r1.counters[0]) + int(r1.counters[8]) == int(r1.frames.sum())
+    assert int(r1.counters[3]) == n * 6 and int(r1.counters[0]) + int(r1.counters[8]) + int(r1.counters[12]) == int(r1.frames.sum())
     # the periodic-rally jump changes nothing: the general kernel simulates every frame
     sel = torch.arange(0, n, 13, device=gpu)
     rg, _ = ev.evaluate(genomes[sel].contiguous(), kind[sel].contiguous(), opp[sel].contiguous(),

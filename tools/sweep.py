@@ -44,6 +44,8 @@ def one(args):
         steps, fwd, slow, fails, plateau, tight = int(c[0]), int(c[1]), int(c[2]), int(c[4]), int(c[5]), int(c[6])
         passes = int(c[7])  # k_wide: network weight passes (each streams one network's genes once)
         c10, c11 = int(c[10]), int(c[11])  # k_wide stamps build: D and prep cycles
+        rally, hidden = int(c[8]), int(c[12])
+        probe = [int(c[13]), int(c[14]), int(c[15])]  # PG_START_PROBE build: start cycles, wave cycles, waves
     mean = sum(ms) / len(ms)
     print(json.dumps({"lib": os.path.basename(os.environ.get("PONG_GA_LIB", "default")), "lanes": args.lane,
                       "kernel": args.kernel,
@@ -51,6 +53,8 @@ def one(args):
                       "env_steps_per_s": steps / (mean / 1e3), "fwd": fwd, "f64_redecide": slow,
                       "cert_fail": fails, "inwave_plateau": tight, "service_certified": plateau,
                       "memo_hits": fails - tight - plateau - slow, "passes": passes, "c10": c10, "c11": c11,
+                      "rally_frames": rally, "hidden_frames": hidden, "start_probe": probe,
+                      "episode_frames_per_s": (steps + rally + hidden) / (mean / 1e3),
                       "stream_TBps": passes * ev.genes * ev.dtype.itemsize / (mean / 1e3) / 1e12}), flush=True)
 
 
