@@ -37,7 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
-PROFILE_ROUND = "r02"           # profiles/<round>/ holds the PMC passes of the committed build
+PROFILE_ROUND = "r03"           # profiles/<round>/ holds the PMC passes of the committed build
 
 
 def parse():
@@ -147,7 +147,8 @@ def main():
     slow_local = 0
     cert_local = [0, 0, 0]  # certificate failures, decided by the service wave, decided in-wave
     passes_local = 0        # k_wide: network weight passes (each streams one network's genes once)
-    skip_local = 0          # episode frames of periodic rallies not simulated (counters[8])
+    skip_local = 0          # episode frames of periodic rallies advanced at once (counters[8])
+    hidden_local = 0        # serve-delay frames advanced at once (counters[12])
     counters = []
     events = []
     for s in range(args.steps):
@@ -172,9 +173,11 @@ def main():
             cert_local[i] += int(c[4 + i])
         passes_local += int(c[7])
         skip_local += int(c[8])
+        hidden_local += int(c[12])
 
     t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)]
-                     + [float(v) for v in cert_local] + [float(passes_local), float(skip_local)],
+                     + [float(v) for v in cert_local] + [float(passes_local), float(skip_local),
+                                                          float(hidden_local)],
                      dtype=torch.float64, device=dev)
     if dist_on:
         tmax = t.clone()
@@ -187,12 +190,14 @@ def main():
         cert_all = [float(v) for v in tsum[5:8]]
         passes_all = float(tsum[8])
         skip_all = float(tsum[9])
+        hidden_all = float(tsum[10])
     else:
         steps_all, fwd_all, slow_all = float(t[1]), float(t[2]), float(t[3])
         kernel_ms_mean = float(t[4]) / args.steps
         cert_all = [float(v) for v in t[5:8]]
         passes_all = float(t[8])
         skip_all = float(t[9])
+        hidden_all = float(t[10])
 
     if rank == 0 and args.config == "wide":
         out = wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all,
@@ -202,12 +207,19 @@ def main():
             cpu_pool.close()
         print(json.dumps(out), flush=True)
     elif rank == 0:
+        # env-steps = every frame of every game played to termination (what the
+        # reference steps env.step through, main.py:76-107): the frames stepped
+        # one at a time plus those advanced in closed form with the identical
+        # outcome (periodic rallies to their timeout, serve delays) -- results
+        # bit-identical to stepping each frame (tests/test_gpu_parity.py)
+        stepped_all = steps_all
+        steps_all = stepped_all + skip_all + hidden_all
         env_steps_per_s = steps_all / elapsed
         ms_per_step = elapsed * 1000.0 / args.steps
-        # roofline of the dominant kernel (k_resident), per launch on rank 0's timing
+        # roofline of the dominant kernel (k_service), per launch on rank 0's timing
         flops_per_forward = 2.0 * G
         fwd_per_launch = fwd_all / world / args.steps
-        steps_per_launch = steps_all / world / args.steps
+        steps_per_launch = stepped_all / world / args.steps
         achieved_tflops = fwd_per_launch * flops_per_forward / (kernel_ms_mean / 1e3) / 1e12
         streaming_bytes = steps_per_launch * (2 * 4 * G + 128)   # SURVEY 8d accounting, GB-equivalent
         out = {
@@ -230,9 +242,13 @@ def main():
                        "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                        "parallelism": f"dp{world}" if world > 1 else "dp1",
                    "process_group": (dist.get_backend() if dist.is_initialized() else None),
+                       "env_steps_definition": "episode frames: every frame of every game to termination; "
+                                               "value = their count / wall time",
                        "env_steps_per_generation": steps_all / args.steps,
-                       "periodic_rally_frames_skipped_per_generation": skip_all / args.steps,
-                       "episode_frames_per_sec_incl_skipped": (steps_all + skip_all) / elapsed,
+                       "stepped_env_steps_per_generation": stepped_all / args.steps,
+                       "stepped_env_steps_per_sec": stepped_all / elapsed,
+                       "periodic_rally_frames_advanced_per_generation": skip_all / args.steps,
+                       "serve_delay_frames_advanced_per_generation": hidden_all / args.steps,
                        "certificate_failures_per_forward": cert_all[0] / max(fwd_all, 1.0),
                        "failures_decided_in_wave": cert_all[2] / max(cert_all[0], 1.0),
                        "failures_decided_by_service_f64_certificate": cert_all[1] / max(cert_all[0], 1.0),
@@ -256,6 +272,9 @@ def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_pe
     wt = 8 if dtype == torch.float64 else 4
     pmc, src = _pmc("pmc_traffic.json")
     traffic = pmc.get("traffic_bytes") if pmc else None
+    stale = _pmc_stale(pmc)
+    if stale:  # counters of another build: not this kernel's traffic
+        traffic = None
     unique = (n_local + H) * G * wt  # every genome row and hall-of-fame row once
     kernel_s = kernel_ms_mean / 1e3
     return {"bound": "valu", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
@@ -265,6 +284,7 @@ def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_pe
             "hbm_frac_of_peak": traffic / kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
             "unique_row_bytes_per_launch": unique,
             "refetch_ratio": traffic / unique if traffic else None,
+            "traffic_stale": stale,
             "traffic_note": "HBM-side bytes per launch (L2 memory-side requests, MALL hits included): rocprofv3 "
                             "FETCH_SIZE + WRITE_SIZE of the same bench command, separate --pmc passes (%s); each "
                             "game loads both networks, so genome rows are fetched ~refetch_ratio times; hbm_GBps = "
@@ -297,9 +317,12 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
     survey_bytes = steps_per_launch * (2 * 4 * G + 128)  # both networks streamed per env-step
     pmc, pmc_src = _pmc("pmc_traffic_wide.json")
     traffic = pmc.get("traffic_bytes_fetch_x2") if pmc else None
+    stale = _pmc_stale(pmc)
+    if stale:
+        traffic = None
     return {
         "metric": "env-steps/sec (GA evaluation loop, self-play, wide MLP) + generations/sec at pop=65536",
-        "value": steps_all / elapsed,
+        "value": (steps_all + skip_all) / elapsed,  # episode frames (periodic rallies advanced at once included)
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -317,12 +340,15 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
                    "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                    "parallelism": f"dp{world}" if world > 1 else "dp1",
                    "process_group": (dist.get_backend() if dist.is_initialized() else None),
-                   "env_steps_per_generation": steps_all / args.steps,
-                   "periodic_rally_frames_skipped_per_generation": skip_all / args.steps,
+                   "env_steps_definition": "episode frames: every frame of every game to termination; "
+                                           "value = their count / wall time",
+                   "env_steps_per_generation": (steps_all + skip_all) / args.steps,
+                   "stepped_env_steps_per_generation": steps_all / args.steps,
+                   "periodic_rally_frames_advanced_per_generation": skip_all / args.steps,
                    "network_passes_per_generation": passes_all / args.steps,
                    "forwards_per_network_pass": fwd_all / max(passes_all, 1.0)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_stale": stale,
                      "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None,
                      "traffic_note": "HBM bytes per launch from the PMC passes (%s): 2 x FETCH_SIZE + WRITE_SIZE "
                                      "(MI355X_MICROARCH.md: on gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane "
@@ -410,7 +436,7 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
 
 def _pmc(name):
     """The newest committed PMC summary of this name (profiles/<round>/), and its path."""
-    for rnd in (PROFILE_ROUND, "r01"):
+    for rnd in (PROFILE_ROUND,):
         path = os.path.join("profiles", rnd, name)
         try:
             with open(os.path.join(REPO, path)) as fh:
@@ -418,6 +444,25 @@ def _pmc(name):
         except (OSError, ValueError):
             continue
     return None, None
+
+
+def _lib_sha():
+    import hashlib
+    from pong_amd import _lib as L
+    with open(L.LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def _pmc_stale(pmc):
+    """None when the committed PMC summary was taken on the library this run
+    loaded; else why not (bench then reports no traffic)."""
+    if not pmc:
+        return "no PMC summary"
+    want = pmc.get("lib_sha256_16")
+    if not want:
+        return "PMC summary names no library build"
+    have = _lib_sha()
+    return None if want == have else f"PMC summary of build {want}, this run loaded {have}"
 
 
 def _pmc_traffic(name="pmc_traffic.json"):

@@ -351,6 +351,10 @@ typedef struct pg_hof_prepare_args {
 
 const char *pg_version(void);
 int32_t pg_abi_version(void);
+/* Build options of this library: bit 0 = the experimental evaluation layouts
+ * (PG_KERNEL_RESIDENT, PG_KERNEL_STAGED) are compiled in; without them those
+ * kernels return PG_ERR_UNSUPPORTED. */
+int32_t pg_build_flags(void);
 const char *pg_last_error(void);
 /* Number of visible HIP devices (>= 0), or a negative pg_status. */
 int32_t pg_device_count(void);

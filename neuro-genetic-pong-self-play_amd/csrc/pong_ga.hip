@@ -182,6 +182,7 @@ __global__ __launch_bounds__(64) void k_general(EvalParams p) {
 
 // (the resident path's and the split path's device helpers live in pg_cascade.hpp)
 
+#ifdef PG_WITH_EXPERIMENTAL  // k_resident: an alternative layout kept out of the product build
 template <int L, int U, int O, typename WT>
 __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
   const int H = p.nodes[1];
@@ -280,6 +281,7 @@ __global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
 }
 
 
+#endif  // PG_WITH_EXPERIMENTAL
 // --------------------------------------------------------------- decide ----
 // k_service's decision cascade on given inputs (pg_decide): the split layout's
 // f32 pass (load_net_pk / partial_pk / group_sum<HL>, the same z and bound e a
@@ -755,6 +757,7 @@ static ResidentChoice choose_resident(int H, int requested_L) {
   return {0, 0};
 }
 
+#ifdef PG_WITH_EXPERIMENTAL
 template <int L, int U, int O, typename WT>
 static int32_t launch_resident(const EvalParams &p, hipStream_t s) {
   constexpr int GPB = 256 / L;
@@ -767,6 +770,8 @@ static int32_t launch_resident(const EvalParams &p, hipStream_t s) {
   PG_HIP(hipGetLastError());
   return PG_OK;
 }
+
+#endif  // PG_WITH_EXPERIMENTAL
 
 // split layout for hidden width H: L lanes per game (L/2 per network).  Fewer
 // lanes per game means more games per wave, so the replicated scalar work of
@@ -799,6 +804,7 @@ static int32_t launch_service_any(const EvalParams &p, int L, int O, hipStream_t
 #endif
 }
 
+#ifdef PG_WITH_EXPERIMENTAL
 template <int L, int U, typename WT>
 static int32_t launch_resident_o(const EvalParams &p, int O, hipStream_t s) {
   switch (O) {
@@ -820,6 +826,7 @@ static int32_t launch_resident_any(const EvalParams &p, ResidentChoice c, int O,
 #undef PG_RES
   return fail(PG_ERR_UNSUPPORTED, "no resident kernel for L=%d U=%d", c.L, c.U);
 }
+#endif  // PG_WITH_EXPERIMENTAL
 
 template <int L, int U, int O, typename WT>
 static int32_t launch_fwd_resident(const FwdParams &p, hipStream_t s) {
@@ -863,6 +870,13 @@ extern "C" {
 
 const char *pg_version(void) { return PG_VERSION_STRING; }
 int32_t pg_abi_version(void) { return PG_ABI_VERSION; }
+int32_t pg_build_flags(void) {
+#ifdef PG_WITH_EXPERIMENTAL
+  return 1;
+#else
+  return 0;
+#endif
+}
 const char *pg_last_error(void) { return g_last_error.c_str(); }
 
 int32_t pg_device_count(void) {
@@ -903,7 +917,9 @@ size_t pg_eval_workspace_bytes(const pg_eval_args *a) {
   if (!a) return n;
   const int kernel = resolve_kernel(a);
   if (kernel == PG_KERNEL_SPLIT) n += split_records_bytes(a);
+#ifdef PG_WITH_EXPERIMENTAL
   if (kernel == PG_KERNEL_STAGED) n += (staged_workspace_bytes(a) + 255) / 256 * 256;
+#endif
   if (kernel == PG_KERNEL_WIDE && wide_shape_ok(a->net, a->n_games)) n += (wide_workspace_bytes(a) + 255) / 256 * 256;
   return n;
 }
@@ -992,7 +1008,17 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     rc = a->net.dtype == PG_F64 ? launch_service_any<double>(p, L, a->net.nodes[2], s)
                                 : launch_service_any<float>(p, L, a->net.nodes[2], s);
     if (rc != PG_OK) return rc;
-  } else if (kernel == PG_KERNEL_RESIDENT) {
+  } else if (kernel == PG_KERNEL_RESIDENT || kernel == PG_KERNEL_STAGED) {
+#ifndef PG_WITH_EXPERIMENTAL
+    return fail(PG_ERR_UNSUPPORTED, "the %s kernel is an experimental layout, not in the product library "
+                "(build with PG_EXPERIMENTAL=1)", kernel == PG_KERNEL_RESIDENT ? "resident" : "staged");
+#else
+    if (kernel == PG_KERNEL_STAGED) {
+      if (!staged_shape_ok(a->net)) return fail(PG_ERR_UNSUPPORTED, "staged kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
+      if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "staged kernel is the certified-precision path");
+      rc = launch_staged(p, a, (char *)a->workspace + eval_base_workspace(a), s);
+      if (rc != PG_OK) return rc;
+    } else {
     if (!res_ok) return fail(PG_ERR_UNSUPPORTED, "resident kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
     if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "resident kernel is the certified-precision path");
     const ResidentChoice c = choose_resident(a->net.nodes[1], a->group_lanes);
@@ -1000,11 +1026,8 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     rc = a->net.dtype == PG_F64 ? launch_resident_any<double>(p, c, a->net.nodes[2], s)
                                 : launch_resident_any<float>(p, c, a->net.nodes[2], s);
     if (rc != PG_OK) return rc;
-  } else if (kernel == PG_KERNEL_STAGED) {
-    if (!staged_shape_ok(a->net)) return fail(PG_ERR_UNSUPPORTED, "staged kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
-    if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "staged kernel is the certified-precision path");
-    rc = launch_staged(p, a, (char *)a->workspace + eval_base_workspace(a), s);
-    if (rc != PG_OK) return rc;
+    }
+#endif
   } else if (kernel == PG_KERNEL_GENERAL) {
     const size_t lds = 2 * (size_t)(p.max_width + 1) * sizeof(double);
     if (lds > 160 * 1024) return fail(PG_ERR_UNSUPPORTED, "layer width %d too large for LDS", p.max_width);

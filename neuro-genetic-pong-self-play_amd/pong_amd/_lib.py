@@ -162,6 +162,7 @@ class PgHofCommitArgs(ctypes.Structure):
 SIGNATURES = {
     "pg_version": (ctypes.c_char_p, []),
     "pg_abi_version": (ctypes.c_int32, []),
+    "pg_build_flags": (ctypes.c_int32, []),
     "pg_last_error": (ctypes.c_char_p, []),
     "pg_device_count": (ctypes.c_int32, []),
     "pg_eval_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PgEvalArgs)]),
@@ -232,6 +233,11 @@ def lib() -> ctypes.CDLL:
                 raise RuntimeError(f"{LIB_PATH}: ABI {L.pg_abi_version()} != {PG_ABI_VERSION}")
             _lib = L
     return _lib
+
+
+def experimental() -> bool:
+    """Whether this library has the experimental layouts (k_resident, k_staged)."""
+    return bool(lib().pg_build_flags() & 1)
 
 
 def check(func: str, rc: int) -> None:

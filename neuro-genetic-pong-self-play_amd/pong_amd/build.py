@@ -10,8 +10,13 @@ from ._lib import LIB_PATH, PKG_DIR, REPO_DIR
 
 CSRC = os.path.join(PKG_DIR, "csrc")
 # one translation unit per kernel family, compiled in parallel and linked into one .so
-SOURCES = [os.path.join(CSRC, f) for f in ("pong_ga.hip", "pg_wide.hip", "pg_pixels.hip", "pg_staged.hip", "pg_service_more.hip", "pg_hof.hip", "pg_gen.hip")]
-DEPS = SOURCES + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp", "pg_cascade.hpp", "pg_service.hpp")] + [
+# PG_EXPERIMENTAL=1 also builds the alternative evaluation layouts k_resident
+# and k_staged (correct, measured slower than k_service), which
+# the product library leaves out; their GPU tests skip without them.
+EXPERIMENTAL = os.environ.get("PG_EXPERIMENTAL") == "1"
+SOURCES = [os.path.join(CSRC, f) for f in ("pong_ga.hip", "pg_wide.hip", "pg_pixels.hip", "pg_service_more.hip",
+                                           "pg_hof.hip", "pg_gen.hip") + (("pg_staged.hip",) if EXPERIMENTAL else ())]
+DEPS = SOURCES + [os.path.join(CSRC, "pg_staged.hip")] + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp", "pg_cascade.hpp", "pg_service.hpp")] + [
     os.path.join(REPO_DIR, "include", "pong_ga.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # per-source flags: the iterative ILP machine scheduler makes k_service's frame
@@ -35,7 +40,8 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB_PATH
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off"] + (
+        ["-DPG_WITH_EXPERIMENTAL"] if EXPERIMENTAL else []) + [
              # no SLP packing of independent f32 adds into v_pk_add_f32: it breaks the
              # DPP-fused reductions into mov_dpp + pk_add pairs (measured -5 %)
              "-fno-slp-vectorize", "-fPIC",

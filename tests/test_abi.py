@@ -81,11 +81,13 @@ def test_validation_errors_without_gpu(lib):
 
 def test_workspace_bytes_follow_the_resolved_kernel(lib):
     """pg_eval_workspace_bytes sizes the kernel the arguments resolve to (host
-    only, no device: the CU count falls back to 256 without a GPU): the split
-    and general kernels need the base (game counter + per-game flags), the
-    wide kernel adds min(n_genomes, CUs) blocks x 7 tile-major W2 copies
-    (config 5 in f32: 1 056 768 B per copy, its tail piece block included),
-    and AUTO resolves like the launch does."""
+    only, no device: the CU count falls back to 256 without a GPU): the
+    general kernel needs the base (game counter + per-game flags), the split
+    kernel adds its lane records (k_prep_records: one per genome and per
+    opponent row, L/2 = 4 lanes x 164 f32 for [6,64,3]), the wide kernel
+    adds min(n_genomes, CUs) blocks x 7 tile-major W2 copies (config 5 in f32:
+    1 056 768 B per copy, its tail piece block included), and AUTO resolves
+    like the launch does."""
     from pong_amd import _lib
     a = _lib.PgEvalArgs()
     a.n_games = 6
@@ -93,7 +95,11 @@ def test_workspace_bytes_follow_the_resolved_kernel(lib):
     a.kernel = _lib.PG_KERNEL_AUTO
     base = 256 + (4096 * 6 * 4 + 255) // 256 * 256
     a.net = _lib.make_net([6, 64, 3])
-    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base
+    rec = 4 * 164 * 4  # 4 lanes x rec_floats<16, 3>() x 4 B per network
+    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base + (4096 * rec + 255) // 256 * 256
+    a.opponents, a.n_opponents = 1, 1024  # (a non-NULL pointer: sizing only)
+    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base + ((4096 + 1024) * rec + 255) // 256 * 256
+    a.opponents, a.n_opponents = None, 0
     a.net = _lib.make_net([6, 512, 512, 3])  # f32 (dtype 0) -> k_wide
     a.net.dtype = _lib.PG_F32
     cus = 256

@@ -164,7 +164,9 @@ def test_eval_matches_oracle(gpu, oracle, shape, dist):
     # simulated env steps + periodic-rally frames not simulated = the episodes' frames
     assert int(res.counters[0]) + int(res.counters[8]) + int(res.counters[12]) == int(ref["frames"].sum())
     if len(shape) == 3:  # the other kernels must agree too
-        for kernel, precision in (("general", "f64"), ("resident", "certified")):
+        from pong_amd import _lib
+        others = (("general", "f64"),) + ((("resident", "certified"),) if _lib.experimental() else ())
+        for kernel, precision in others:
             res2, _ = ev.evaluate(_dev_genomes(genomes, gpu), torch.tensor(kinds, device=gpu),
                                   torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
                                   opponents=_dev_genomes(opponents, gpu), kernel=kernel, precision=precision)
@@ -180,6 +182,9 @@ def test_eval_matches_oracle(gpu, oracle, shape, dist):
 def test_eval_kernel_layouts(gpu, oracle, kernel, lanes, hidden):
     """Every lane layout of both register-resident kernels vs the oracle."""
     from pong_amd.device import Evaluator
+    if kernel == "resident":
+        from conftest import need_experimental
+        need_experimental()
     shape = [6, hidden, 3]
     rng = np.random.default_rng(lanes * 1000 + hidden)
     G = _gene_count(shape)
@@ -264,6 +269,9 @@ def test_episode_traces_match_reference(gpu, golden, name, kernel):
     2 000-frame timeouts), traced; then untraced, where the kernels jump over
     periodic rallies -- frames, scores and rewards must not change."""
     from pong_amd.device import Evaluator
+    if kernel == "staged":
+        from conftest import need_experimental
+        need_experimental()
     eps = golden(name)
     for ep in eps:
         shape = ep["shape"]

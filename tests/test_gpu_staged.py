@@ -16,6 +16,12 @@ from test_gpu_parity import _assert_same, _dev_genomes, _gene_count, _run_both, 
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _experimental_build(gpu):
+    from conftest import need_experimental
+    need_experimental()
+
+
 @pytest.mark.parametrize("shape", [[6, 2, 2], [6, 8, 3], [6, 37, 3], [6, 64, 3], [6, 64, 2], [6, 64, 4],
                                    [6, 100, 3], [6, 200, 4]])
 @pytest.mark.parametrize("dist", ["init", "n3"])

@@ -15,7 +15,7 @@ SFLAG=""; [ -n "$SCHED" ] && SFLAG="-mllvm -amdgpu-sched-strategy=$SCHED"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -Wall \
   -Wno-unused-function -I $ROOT/include $SFLAG "$@" -c -o /tmp/pg_variant_$NAME.o $C/$TU
 OBJS=""
-for t in pong_ga pg_wide pg_pixels pg_staged pg_service_more pg_hof pg_gen; do
+for t in pong_ga pg_wide pg_pixels pg_service_more pg_hof pg_gen; do
   if [ "$t.hip" = "$TU" ]; then OBJS="$OBJS /tmp/pg_variant_$NAME.o"; else OBJS="$OBJS $C/$t.o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $ROOT/variants/lib_$NAME.so $OBJS

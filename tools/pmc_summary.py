@@ -13,7 +13,9 @@ for tag in sys.argv[1:]:
             if any(k in r["Kernel_Name"] for k in ("k_resident", "k_split", "k_service")):
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
         try:
-            steps = json.loads(open(f"{tag}/{p}.out").read().strip().splitlines()[-1])["env_steps"]
+            js = json.loads(open(f"{tag}/{p}.out").read().strip().splitlines()[-1])
+            steps = js["env_steps"]
+            episode = steps + js.get("rally_frames", 0) + js.get("hidden_frames", 0)
         except Exception:
             pass
     d = {k: v[-1] for k, v in vals.items()}
@@ -24,3 +26,5 @@ for tag in sys.argv[1:]:
     print("  wave-cycle shares: wait_any %.2f wait_inst_any %.2f active_any %.2f active_valu %.2f active_sca %.2f" % tuple(
         d[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA")))
     print("  busy cycles %.3g, wave-cycles per step %.1f" % (d["SQ_BUSY_CYCLES"], wc / steps))
+    print("  per episode frame (%d): VALU %.1f SALU %.1f" % (episode, d["SQ_INSTS_VALU"] / episode,
+                                                             d["SQ_INSTS_SALU"] / episode))

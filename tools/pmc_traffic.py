@@ -23,6 +23,17 @@ def mean_counter(path, name, kernel="k_service"):
     return sum(vals) / len(vals), len(vals), sum(durs) / len(durs)
 
 
+def lib_sha(path=None):
+    """sha256 (16 hex digits) of the library the passes ran: bench.py reports
+    the traffic only while it runs the same build."""
+    import hashlib
+    import os
+    path = path or os.environ.get("PONG_GA_LIB") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "neuro-genetic-pong-self-play_amd", "libpong_ga.so")
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
 def main():
     run, out = sys.argv[1], sys.argv[2]
     kernel = sys.argv[3] if len(sys.argv) > 3 else "k_service"
@@ -37,7 +48,7 @@ def main():
            "traffic_bytes_fetch_x2": (2 * fetch + write) * kib,
            "dispatch_ms": dur_s * 1e3,
            "hbm_GBps": traffic / dur_s / 1e9,
-           "source": run}
+           "source": run, "lib_sha256_16": lib_sha()}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
