@@ -26,6 +26,7 @@
  * pg_forward                     NeuralNetwork.run numpy_nn.py:120-137 (batched)
  * pg_decide                      get_actions' model.run argmax (main.py:143-150) as the
  *                                hot kernel decides it (test / fixture entry point)
+ * pg_wide_decide                 the same, as k_wide decides it (config 5 networks)
  * pg_physics_reset/pg_physics_step  env.reset()/env.step(action) main.py:56,77
  *                                (the build's SoA Pong; the emulator is absent)
  * pg_ga_select_tournament        tools.selTournament (ga.py:94; DEAP)
@@ -65,7 +66,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 5
+#define PG_ABI_VERSION 6
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -212,6 +213,25 @@ typedef struct pg_decide_args {
   int32_t *stage;                /* optional out [n]: 0 f32 certificate, 1 in-wave plateau rule,
                                     2 service wave's certified rules, 3 numpy-order f64 forward */
 } pg_decide_args;
+
+/* The wide kernel's decision for given inputs: k_wide itself (the evaluation
+ * kernel of [6, H1 <= 512, H2 <= 512, 1..4] networks, BASELINE config 5) runs
+ * one frame of network row genome_index[i] (i if NULL) on the doubled
+ * centroids k[i][0..5] -- its layer path and argmax exactly as in a game
+ * (get_actions main.py:143-150, NeuralNetwork.run numpy_nn.py:120-137), so the
+ * near-tie fixtures k_wide logs (pg_eval_args.hard_log) pin k_wide itself. */
+typedef struct pg_wide_decide_args {
+  pg_net net;
+  int32_t n;
+  const void *genomes;           /* [*, genome_stride] (net.dtype) */
+  int64_t genome_stride;
+  const int32_t *genome_index;   /* [n] or NULL */
+  const int32_t *k;              /* [n, 6] doubled centroids, each in [0, 320] */
+  int32_t *index;                /* out [n] np.argmax of NeuralNetwork.run's activations */
+  double *act;                   /* optional out [n, nodes[3]] the output activations */
+  void *workspace;               /* device, pg_wide_decide_workspace_bytes */
+  size_t workspace_bytes;
+} pg_wide_decide_args;
 
 /* Struct-of-arrays game state: int32 [PG_STATE_FIELDS, n], field f of game i
  * at state[f * n + i]; 64 bytes per game. */
@@ -364,6 +384,8 @@ int32_t pg_gene_count(const pg_net *net);
 int32_t pg_eval_population(const pg_eval_args *args, void *stream);
 int32_t pg_forward(const pg_forward_args *args, void *stream);
 int32_t pg_decide(const pg_decide_args *args, void *stream);
+size_t pg_wide_decide_workspace_bytes(const pg_wide_decide_args *args);
+int32_t pg_wide_decide(const pg_wide_decide_args *args, void *stream);
 int32_t pg_physics_reset(int32_t *state, int32_t n, const uint64_t *seeds,
                          const int32_t *one_player, void *stream);
 /* actions [n]: bit0 right up, bit1 right down, bit2 left up, bit3 left down */

@@ -49,6 +49,11 @@ struct EvalParams {
   float *recs;         // split kernel: lane records (k_prep_records), [n_genomes + n_opponents][L/2][rec_floats]
   void *wide_scratch;  // k_wide: the blocks' tile-major W2 copies (workspace)
   int wide_w3_resident;  // k_wide: every network's W3 kept in LDS for the genome's games
+  // k_wide probe (pg_wide_decide, n_games = 1): block i runs one frame of
+  // genome i on the doubled centroids wide_probe_k[i][0..5] instead of a game
+  const int32_t *wide_probe_k;
+  int32_t *wide_probe_index;  // out [n_genomes] np.argmax
+  double *wide_probe_act;     // optional out [n_genomes, nodes[3]]
 };
 
 // Genome blocks / games this launch plays (pg_eval_args.n_active).  Made

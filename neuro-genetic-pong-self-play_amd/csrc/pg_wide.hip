@@ -250,6 +250,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
   const int n_games = p.n_games;
+  const bool probe = p.wide_probe_k != nullptr;  // pg_wide_decide (n_games = 1)
   uint64_t c_steps = 0, c_fwd = 0, c_games = 0, c_streams = 0, c_skip = 0;
   const int n_genomes_active = active_genomes(p);
 
@@ -267,7 +268,9 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
     bool active = false;
     if (wid == 0 && lane < n_games) {
       w = gi * n_games + lane;
-      kind = p.kind[w];
+      // probe (pg_wide_decide): one scripted-opponent "game" whose single frame
+      // is the genome on the given features
+      kind = probe ? kOppHard : p.kind[w];
       orow[lane] = kind == kOppNN ? (long long)p.opp[w] * p.ostride : 0;
       st.reset(game_seed(p.seed, lane), kind == kOppRomCpu);
       active = true;
@@ -284,7 +287,14 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       // ---- A: env.step + find_stuff + inference features (main.py:77-87)
       int s1b = 0, s2b = 0, vis = 0, lc2 = 0, rc2 = 0, left = 0;
       if (wid == 0) {
-        if (active) {
+        if (active && probe) {  // the given doubled centroids (log_wide's k) in place of a frame
+          vis = 1;
+          const int32_t *kk = p.wide_probe_k + (long)gi * 6;
+          double *fr = feat + lane * 8;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) fr[i] = feat64(kk[i]);
+          fr[6] = 1.0;
+        } else if (active) {
           s1b = st.s1;
           s2b = st.s2;
           const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
@@ -677,7 +687,12 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       }
 
       // ---- E: actions, clamp, bookkeeping (main.py:88-107, 128-135)
-      if (wid == 0 && active) {
+      if (wid == 0 && active && probe) {
+        p.wide_probe_index[gi] = argmax_np(outv, O);
+        if (p.wide_probe_act)
+          for (int o = 0; o < O; ++o) p.wide_probe_act[(long)gi * O + o] = outv[o];
+        active = false;
+      } else if (wid == 0 && active) {
         int right = 0;
         if (vis) {
           const int ir = argmax_np(outv + lane * 4, O);

@@ -1148,6 +1148,60 @@ int32_t pg_decide(const pg_decide_args *a, void *stream) {
   return fail(PG_ERR_UNSUPPORTED, "pg_decide: no layout for H=%d", H);
 }
 
+// pg_wide_decide runs k_wide as a one-game evaluation of n genomes: the
+// evaluation's sizes for its workspace (a game counter, then the blocks' W2 copies)
+static pg_eval_args wide_decide_eval(const pg_wide_decide_args *a) {
+  pg_eval_args e;
+  memset(&e, 0, sizeof(e));
+  e.net = a->net;
+  e.n_genomes = a->n;
+  e.n_games = 1;
+  return e;
+}
+
+size_t pg_wide_decide_workspace_bytes(const pg_wide_decide_args *a) {
+  if (!a || a->n <= 0 || !wide_shape_ok(a->net, 1)) return 256;
+  const pg_eval_args e = wide_decide_eval(a);
+  return 256 + (wide_workspace_bytes(&e) + 255) / 256 * 256;
+}
+
+int32_t pg_wide_decide(const pg_wide_decide_args *a, void *stream) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  int32_t rc = check_net(a->net, false);
+  if (rc != PG_OK) return rc;
+  if (!wide_shape_ok(a->net, 1))
+    return fail(PG_ERR_UNSUPPORTED, "pg_wide_decide: the wide kernel's shapes [6, H1<=512, H2<=512, 1..4] only");
+  if (a->n < 0) return fail(PG_ERR_INVALID, "n=%d < 0", a->n);
+  if (a->n == 0) return PG_OK;
+  const int G = gene_count(a->net);
+  if (!a->genomes || a->genome_stride < G || !a->k || !a->index)
+    return fail(PG_ERR_INVALID, "genomes/k/index NULL or genome_stride < gene count %d", G);
+  const size_t need = pg_wide_decide_workspace_bytes(a);
+  if (!a->workspace || a->workspace_bytes < need)
+    return fail(PG_ERR_INVALID, "workspace of %zu bytes required (got %zu)", need, a->workspace_bytes);
+  hipStream_t s = (hipStream_t)stream;
+  EvalParams p;
+  memset(&p, 0, sizeof(p));
+  p.genomes = a->genomes;
+  p.opponents = a->genomes;
+  p.rows = a->genome_index;
+  p.work = (unsigned int *)a->workspace;
+  p.gstride = a->genome_stride;
+  p.ostride = a->genome_stride;
+  p.n_genomes = a->n;
+  p.n_games = 1;
+  p.total = a->n;
+  for (int i = 0; i < a->net.n_nodes; ++i) p.nodes[i] = a->net.nodes[i];
+  p.n_nodes = a->net.n_nodes;
+  p.bias = a->net.bias ? 1 : 0;
+  p.max_width = max_width(a->net);
+  p.wide_probe_k = a->k;
+  p.wide_probe_index = a->index;
+  p.wide_probe_act = a->act;
+  PG_HIP(hipMemsetAsync(a->workspace, 0, 256, s));
+  return launch_wide(p, a->net.dtype, (char *)a->workspace + 256, s);
+}
+
 int32_t pg_physics_reset(int32_t *state, int32_t n, const uint64_t *seeds, const int32_t *one_player,
                          void *stream) {
   if (n < 0 || (n > 0 && !state)) return fail(PG_ERR_INVALID, "state NULL or n < 0");

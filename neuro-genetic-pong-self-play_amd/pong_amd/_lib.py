@@ -16,7 +16,7 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 5
+PG_ABI_VERSION = 6
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -69,6 +69,14 @@ class PgDecideArgs(ctypes.Structure):
     _fields_ = [
         ("net", PgNet), ("n", ctypes.c_int32), ("genomes", _vp), ("genome_stride", ctypes.c_int64),
         ("genome_index", _vp), ("k", _vp), ("index", _vp), ("stage", _vp),
+    ]
+
+
+class PgWideDecideArgs(ctypes.Structure):
+    _fields_ = [
+        ("net", PgNet), ("n", ctypes.c_int32), ("genomes", _vp), ("genome_stride", ctypes.c_int64),
+        ("genome_index", _vp), ("k", _vp), ("index", _vp), ("act", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
     ]
 
 
@@ -170,6 +178,8 @@ SIGNATURES = {
     "pg_eval_population": (ctypes.c_int32, [ctypes.POINTER(PgEvalArgs), _vp]),
     "pg_forward": (ctypes.c_int32, [ctypes.POINTER(PgForwardArgs), _vp]),
     "pg_decide": (ctypes.c_int32, [ctypes.POINTER(PgDecideArgs), _vp]),
+    "pg_wide_decide_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PgWideDecideArgs)]),
+    "pg_wide_decide": (ctypes.c_int32, [ctypes.POINTER(PgWideDecideArgs), _vp]),
     "pg_physics_reset": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp, _vp]),
     "pg_physics_step": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp]),
     "pg_ga_select_tournament": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp]),

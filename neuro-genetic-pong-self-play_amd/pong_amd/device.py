@@ -259,6 +259,34 @@ class Evaluator:
             L.check("pg_decide", L.lib().pg_decide(ctypes.byref(a), _stream(dev)))
         return index, stage
 
+    def wide_decide(self, genomes: torch.Tensor, k: torch.Tensor, genome_index: Optional[torch.Tensor] = None):
+        """k_wide's own decision (pg_wide_decide: one frame of the evaluation
+        kernel per pass) on doubled-centroid features k [n, 6] int32: returns
+        (argmax index [n] int32, output activations [n, out] f64)."""
+        dev = self.device
+        _need(genomes, "genomes", self.dtype, dev)
+        n = k.shape[0]
+        _need(k, "k", torch.int32, dev, (n, 6))
+        if genome_index is not None:
+            _need(genome_index, "genome_index", torch.int32, dev, (n,))
+        index = torch.empty(n, dtype=torch.int32, device=dev)
+        act = torch.empty((n, self.nodes[-1]), dtype=torch.float64, device=dev)
+        a = L.PgWideDecideArgs()
+        a.net = self.net
+        a.n = n
+        a.genomes = _ptr(genomes)
+        a.genome_stride = genomes.stride(0) if genomes.shape[0] > 1 else genomes.shape[1]
+        a.genome_index = _ptr(genome_index)
+        a.k = _ptr(k)
+        a.index = _ptr(index)
+        a.act = _ptr(act)
+        nbytes = L.lib().pg_wide_decide_workspace_bytes(ctypes.byref(a))
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = _ptr(ws), nbytes
+        with torch.cuda.device(dev):
+            L.check("pg_wide_decide", L.lib().pg_wide_decide(ctypes.byref(a), _stream(dev)))
+        return index, act
+
 
 class Physics:
     """The SoA Pong stepper (pg_physics_reset / pg_physics_step) for n games."""

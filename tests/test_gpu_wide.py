@@ -138,3 +138,66 @@ def test_wide_selfplay_properties(gpu):
                         mult[sel].contiguous(), opponents=opponents, kernel="general")
     assert torch.equal(rg.fitness, r1.fitness[sel]) and torch.equal(rg.frames, r1.frames[sel])
     assert torch.equal(rg.scores, r1.scores[sel]) and torch.equal(rg.total_frames, r1.total_frames[sel])
+
+
+def test_wide_config5_pop4096(gpu, oracle):
+    """Config 5 at pop 4 096 ([6, 512, 512, 3], f32 genome storage, self-play
+    schedule of BASELINE configs[4] against 1 024 hall-of-fame rows): every
+    game ends and is counted, results are permutation-equivariant, a few
+    genomes' whole evaluations equal the oracle's, and every decision k_wide
+    logged as a near-tie (top two activations within 1e-12) is the oracle's
+    numpy-order argmax (numpy_nn.py:126-131) and k_wide's own pg_wide_decide."""
+    from pong_amd.device import Evaluator
+    shape = [6, 512, 512, 3]
+    G = _gene_count(shape)
+    n, H = 4096, 1024
+    gen = torch.Generator(device=gpu).manual_seed(4096)
+    genomes = torch.randn((n, G), generator=gen, dtype=torch.float32, device=gpu) * 3.0
+    opponents = torch.randn((H, G), generator=gen, dtype=torch.float32, device=gpu) * 3.0
+    ev = Evaluator(shape, dtype=torch.float32, device=gpu)
+    kind, opp, mult = ev.selfplay_schedule(n, H)
+    cap = 4096
+    hard = torch.zeros((cap, 8), dtype=torch.int32, device=gpu)
+    r1, _ = ev.evaluate(genomes, kind, opp, mult, opponents=opponents, hard_log=hard)
+    torch.cuda.synchronize()
+    c = r1.counters.cpu().numpy()
+    assert int(c[3]) == n * 6 and int(c[0]) + int(c[8]) + int(c[12]) == int(r1.frames.sum())
+    assert int(r1.status.sum()) == 0 and bool(torch.isfinite(r1.fitness).all())
+    assert int(r1.frames.min()) >= 1
+    # permutation-equivariant
+    perm = torch.randperm(n, device=gpu, generator=torch.Generator(device=gpu).manual_seed(1))
+    r2, _ = ev.evaluate(genomes[perm].contiguous(), kind[perm].contiguous(), opp[perm].contiguous(),
+                        mult[perm].contiguous(), opponents=opponents)
+    assert torch.equal(r2.fitness, r1.fitness[perm]) and torch.equal(r2.frames, r1.frames[perm])
+    assert torch.equal(r2.scores, r1.scores[perm])
+    # oracle re-check of four genomes: the first, the last, the longest and the fittest
+    pick = sorted({0, n - 1, int(r1.frames.sum(dim=1).argmax()), int(r1.fitness.argmax())})
+    sel = torch.tensor(pick, device=gpu)
+    o_rows = torch.unique(opp[sel].flatten())
+    remap = torch.full((H,), -1, dtype=torch.int32, device=gpu)
+    remap[o_rows] = torch.arange(len(o_rows), dtype=torch.int32, device=gpu)
+    ref = oracle.eval_population(genomes[sel].double().cpu().numpy(), shape, kind[sel].cpu().numpy(),
+                                 remap[opp[sel].long()].cpu().numpy(), mult[sel].cpu().numpy(),
+                                 opponents=opponents[o_rows].double().cpu().numpy(), n_threads=8)
+    for name in ("scores", "frames", "total_frames", "rewards", "fitness"):
+        np.testing.assert_array_equal(getattr(r1, name)[sel].cpu().numpy(), ref[name], err_msg=name)
+    # the near-ties: the oracle's forward, and k_wide's own decision on the same input
+    k = min(int(c[9]), cap)
+    print(f"config 5 pop {n}: {int(c[0])} stepped + {int(c[8]) + int(c[12])} advanced frames, {int(c[9])} near-ties")
+    if k:
+        log = hard[:k].cpu().numpy()
+        row, is_opp, idx = log[:, 0], log[:, 1] & 1, (log[:, 1] >> 8) & 255
+        kk = log[:, 2:8].astype(np.int32)
+        use = np.arange(k)[:512]
+        for i in use:
+            net = (opponents if is_opp[i] else genomes)[int(row[i])].double().cpu().numpy()
+            oi, _ = oracle.nn_run(net, shape, (kk[i].astype(np.float64) / 2) / 160)
+            assert oi == idx[i], (i, oi, idx[i])
+        # pg_wide_decide on genome rows / opponent rows separately
+        for flag, table in ((0, genomes), (1, opponents)):
+            m = is_opp[use] == flag
+            if not m.any():
+                continue
+            rows_t = torch.tensor(row[use][m], dtype=torch.int32, device=gpu)
+            wi, _ = ev.wide_decide(table, torch.tensor(kk[use][m], device=gpu), genome_index=rows_t)
+            np.testing.assert_array_equal(wi.cpu().numpy(), idx[use][m])
