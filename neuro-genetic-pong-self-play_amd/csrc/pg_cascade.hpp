@@ -365,32 +365,46 @@ __device__ __forceinline__ int certify(const float z[O], float e) {
   // surely is (it ties at 1.0 with every later saturated one and beats every
   // unsaturated one); (b) with none possibly saturated, the f32 winner must
   // lead the runner-up by 2e plus the plateau width at its value.
+  // The thresholds move by e once instead of every z by e: z >= kTlo - e
+  // "may be saturated", z > kThi + e "surely is" (the f32 rounding of either
+  // form is ~1e-6 of the 1e-4 margins around 53 ln 2 and within the bound's x2
+  // slack).  An infinite e (weights_ok failed) makes every output "maybe" and
+  // none "sure": -1.
   constexpr float kTlo = 36.7367f, kThi = 36.7369f;
   constexpr float kLowZ = -708.0f;
-  int sat_res = -2;  // -2: no output may be saturated
+  const float tlo = kTlo - e, thi = kThi + e;
+  // (a) the first maybe-saturated output decides if it surely is (a sure
+  // output is a maybe one), else -1
+  int sat_res = z[O - 1] > thi ? O - 1 : -1;
 #pragma unroll
-  for (int o = O - 1; o >= 0; --o) {
-    const bool maybe = !(z[o] + e < kTlo);  // NaN counts as "maybe"
-    const bool sure = z[o] - e > kThi;
-    sat_res = maybe ? (sure ? o : -1) : sat_res;
-  }
-  float top1 = z[0], top2 = -3.0e38f;
-  int w = 0;
+  for (int o = O - 2; o >= 0; --o) sat_res = z[o] > thi ? o : (z[o] >= tlo ? -1 : sat_res);
+  float top1, top2;
+  int w;
+  if constexpr (O == 3) {  // v_max3 / v_med3: the largest and the runner-up (equal to it on a tie)
+    top1 = fmaxf(fmaxf(z[0], z[1]), z[2]);
+    top2 = __builtin_amdgcn_fmed3f(z[0], z[1], z[2]);
+    w = z[0] == top1 ? 0 : (z[1] == top1 ? 1 : 2);
+  } else {
+    top1 = z[0];
+    top2 = -3.0e38f;
+    w = 0;
 #pragma unroll
-  for (int o = 1; o < O; ++o) {
-    const bool gt = z[o] > top1;
-    top2 = gt ? top1 : fmaxf(top2, z[o]);
-    w = gt ? o : w;
-    top1 = gt ? z[o] : top1;
+    for (int o = 1; o < O; ++o) {
+      const bool gt = z[o] > top1;
+      top2 = gt ? top1 : fmaxf(top2, z[o]);
+      w = gt ? o : w;
+      top1 = gt ? z[o] : top1;
+    }
   }
   // (top1 + e < kTlo whenever this rule is used: no saturated output)
   const float tw = 8.8817842e-16f * (__expf(top1 + e) + 1.0f);
   // the gap rule needs the winner's S(z) normal: below z = -1022 ln 2 it is
   // subnormal (coarse steps), and 0.0 for every z < -709.78 (pow overflows),
   // where all such outputs tie and the first wins -- the f64 path decides there
-  const int uns_res = (top1 - top2 > 2.f * e + tw && top1 - e > kLowZ) ? w : -1;
-  // no NaN test: outputs are finite whenever e is (weights_ok at load time)
-  return sat_res != -2 ? sat_res : uns_res;
+  const int uns_res = (top1 - top2 > 2.f * e + tw && top1 > kLowZ + e) ? w : -1;
+  // no NaN test: outputs are finite whenever e is (weights_ok at load time);
+  // the largest output maybe-saturated <=> some output is
+  return top1 >= tlo ? sat_res : uns_res;
 }
 
 // The f64 re-decision of one forward pass by the L lanes of a group, in
