@@ -181,9 +181,10 @@ __device__ inline uint64_t rally_key(const Pong &s, int act_r, int act_l) {
   return k;
 }
 // Brent's cycle search over one point: the key is saved when the no-score
-// counter reaches kRallyStart and re-saved each time the distance doubles;
-// keys are compared every kRallyStride frames (a multiple of the period is
-// then still met within kRallyStride periods).
+// counter reaches kRallyStart and re-saved each time the distance doubles.
+// k_wide compares keys every kRallyStride frames (a multiple of the period is
+// then still met within kRallyStride periods); k_service at the frames where
+// a paddle returns the ball (pg_service.hpp).
 #ifndef PG_RALLY_START
 #define PG_RALLY_START 256
 #endif

@@ -146,6 +146,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   uint64_t t_start = 0;
   uint32_t g_fails = 0, g_slow = 0;
 #endif
+#ifdef PG_PATH_PROBE  // diagnostic build: wave-frames that take each rare path (any game of the wave)
+  uint32_t pp_frames = 0, pp_rally = 0, pp_face = 0, pp_fail = 0, pp_hidden = 0;
+#define PG_PP(cnt, cond) \
+  if (__builtin_amdgcn_ballot_w64(cond) != 0) cnt += 1
+#else
+#define PG_PP(cnt, cond)
+#endif
   while (w < games_total) {
 #ifdef PG_START_PROBE
     const bool any_fresh = __builtin_amdgcn_ballot_w64(fresh) != 0;
@@ -164,9 +171,11 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       gm = nn ? opponents + (long)oj * p.ostride : gr;
       load_rec<U, O>(net, p.recs + ((nn ? (long)p.n_genomes + oj : (long)i) * HL + hl) * rec_floats<U, O>());
       st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
-      act_r = act_l = timeout = total = frames = 0;
+      act_r = act_l = total = frames = 0;
+      timeout = -1;  // frame 1 does not count (main.py:94-96): it takes the counter to 0
       fresh = false;
       if (hl == 0) slots[sx].n_memo = 0;
+      if (lig == 0) slots[sx].rally_at = -1;  // (sx is the side-0 slot there)
 #ifdef PG_TIMELINE  // experiment build: per-game wall-clock start/end into p.trace
       t_start = wall_clock64();
       g_fails = g_slow = 0;
@@ -188,15 +197,17 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #else
       const bool kTrace = p.trace != nullptr;
 #endif
-      const bool hid = !kTrace && !st.vis && st.timer >= 2;
-      if (__builtin_amdgcn_ballot_w64(hid) != 0 && hid) {
+      const bool hid = !st.vis && st.timer >= 2;
+      PG_PP(pp_hidden, hid);
+      PG_PP(pp_frames, true);
+      if (!kTrace && __builtin_amdgcn_ballot_w64(st.vis == 0) != 0 && hid) {
         const int h = st.timer - 1;
         st.rpy = Pong::drift(st.rpy, h);
         if (!st.one_player) st.lpy = Pong::drift(st.lpy, h);
         st.timer = 1;
         act_r = clamp_action(paddle_c2(st.rpy), 0);
         act_l = clamp_action(paddle_c2(st.lpy), 0);
-        timeout += frames > 0 ? h : h - 1;  // frame 1 of a game does not count (main.py:94-96)
+        timeout += h;
         frames += h;
         hidden += h;
       }
@@ -204,7 +215,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #endif
     const int s1b = st.s1, s2b = st.s2;
     const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
+    const int hits_b = st.hits;
+#ifdef PG_PATH_PROBE
+    const int pt_b = st.point;
+#endif
     st.step(act_r, act_l);
+    const bool bounced = st.hits != hits_b;  // a paddle returned the ball this frame
+    PG_PP(pp_face, st.hits != hits_b || st.s1 != s1b || st.s2 != s2b || st.point != pt_b);
     frames += 1;
     const int vis = st.vis;
     const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
@@ -225,6 +242,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
       if (idx < 0) idx = z[1] > z[0] ? 1 : 0;
 #endif
+      PG_PP(pp_fail, idx < 0);
       if (idx < 0) {  // rare, half-uniform: the memo, else ask the service wave
         fails += 1;
 #ifdef PG_TIMELINE
@@ -293,13 +311,11 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
     }
 #endif
-    if (frames > 1) {
-      if (st.s1 == s1b && st.s2 == s2b) {
-        timeout += 1;
-      } else {
-        total += timeout;
-        timeout = 0;
-      }
+    {  // calculate_timeout_and_frames (main.py:128-135); at most one point a frame
+      const bool same = st.s1 + st.s2 == s1b + s2b;
+      total += same ? 0 : timeout;
+      timeout = same ? timeout + 1 : 0;
+      if (!same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
     }
 #ifndef PG_NO_RALLY_SKIP
     // a periodic rally ends at the timeout with nothing else changed: jump there
@@ -309,11 +325,20 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #else
     const bool kTracing = p.trace != nullptr;
 #endif
-    if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
-        !kTracing) {
+    // Brent's cycle search sampled at the frames where a paddle returned the
+    // ball (the states at the bounces of a periodic rally repeat too): the
+    // first bounce past kRallyStart opens the rally's search (a point or a
+    // game start clears the save), a later bounce state equal to the saved one
+    // proves the rally periodic, and the save moves forward when the distance
+    // reaches the span, which doubles.  Sampling at bounces instead of every
+    // kRallyStride frames: 15 % -> 2 % of wave-frames build a key
+    // (profiles/r03/sweep_frame_trims_g5.log).
+    PG_PP(pp_rally, bounced && timeout >= kRallyStart && timeout <= kTimeoutThresh);
+    if (bounced && timeout >= kRallyStart && timeout <= kTimeoutThresh && !kTracing) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
       const uint64_t key = rally_key(st, act_r, act_l);
-      if (timeout == kRallyStart) {
+      const int at = slots[rs].rally_at;
+      if (at > timeout || at < 0) {
         if (lig == 0) {
           slots[rs].rally_key = key;
           slots[rs].rally_at = timeout;
@@ -324,7 +349,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         frames += rest;
         skipped += rest;
         timeout = kTimeoutThresh + 1;
-      } else if (timeout - slots[rs].rally_at == slots[rs].rally_span) {
+      } else if (timeout - at >= slots[rs].rally_span) {
         if (lig == 0) {
           slots[rs].rally_key = key;
           slots[rs].rally_at = timeout;
@@ -376,6 +401,15 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     atomicAdd((unsigned long long *)&p.counters[13], (unsigned long long)probe_fresh);
     atomicAdd((unsigned long long *)&p.counters[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - probe_t0));
     atomicAdd((unsigned long long *)&p.counters[15], 1ull);
+  }
+#endif
+#ifdef PG_PATH_PROBE
+  if (p.counters && lane64 == 0) {
+    atomicAdd((unsigned long long *)&p.counters[11], (unsigned long long)pp_frames);
+    atomicAdd((unsigned long long *)&p.counters[10], (unsigned long long)pp_rally);
+    atomicAdd((unsigned long long *)&p.counters[13], (unsigned long long)pp_face);
+    atomicAdd((unsigned long long *)&p.counters[14], (unsigned long long)pp_fail);
+    atomicAdd((unsigned long long *)&p.counters[15], (unsigned long long)pp_hidden);
   }
 #endif
   // this wave will post no more requests
