@@ -67,8 +67,24 @@ struct Pong {
   __device__ static int dy_of(int code) {  // code: 0 = [0,0], 1 = [1,0] up, 2 = [0,1] down, 3 = [1,1]
     return (code == 2) - (code == 1);
   }
-  __device__ static int move(int y, int dy, int speed) {
-    return min(max(y + dy * speed, kPaddleYMin), kPaddleYMax);  // one v_med3_i32
+  // the row clamp of a paddle top: one v_med3_i32 (the upper bound from an
+  // SGPR: a gfx9 VOP3 takes no literal, so min(max()) compiled to two ops)
+  __device__ static int clamp_row(int y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int r;
+    asm("v_med3_i32 %0, %1, -8, %2" : "=v"(r) : "v"(y), "s"(kPaddleYMax));
+    static_assert(kPaddleYMin == -8, "the inline constant above");
+    return r;
+#else
+    return min(max(y, kPaddleYMin), kPaddleYMax);
+#endif
+  }
+  __device__ static int move(int y, int dy, int speed) { return clamp_row(y + dy * speed); }
+  // a player's move for action code c: 0, -3, +3, 0 rows (dy_of(c) * kPaddleSpeed
+  // as one signed bitfield extract from a byte table)
+  __device__ static int move_player(int y, int code) {
+    static_assert(kPaddleSpeed == 3, "the table below");
+    return clamp_row(y + __builtin_amdgcn_sbfe(0x0003FD00, 8 * code, 8));
   }
 
   // env.step(action) (main.py:77): right [up,down] = action[4:6], left = action[6:8].
@@ -77,15 +93,16 @@ struct Pong {
   // game) and the hidden-ball countdown are branches.  The lanes of a group
   // play one game, so a branch only costs the waves where some game takes it.
   __device__ void step(int right_code, int left_code) {
-    rpy = move(rpy, dy_of(right_code), kPaddleSpeed);
+    rpy = move_player(rpy, right_code);
     // left paddle: the action, or the built-in CPU of the 1-player env
-    // (main.py:40) -- a branch: no game of a self-play schedule takes it
-    if (__builtin_expect(one_player, 0)) {
+    // (main.py:40) -- behind a wave-uniform test: no game of a self-play
+    // schedule takes it
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(one_player != 0) != 0, 0)) {
       const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
       const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
-      lpy = move(lpy, cpu_dy, kCpuSpeed);
+      lpy = one_player ? move(lpy, cpu_dy, kCpuSpeed) : move_player(lpy, left_code);
     } else {
-      lpy = move(lpy, dy_of(left_code), kPaddleSpeed);
+      lpy = move_player(lpy, left_code);
     }
 
     constexpr int ymax = kFieldH - kBallH;
@@ -215,7 +232,9 @@ __device__ inline int hardcoded(int by2, int me2) { return by2 < me2 ? 1 : (by2 
 
 // argmax index -> action code (numpy_nn.py:131-137; index >= 2 -> no-op, the
 // build's extension for 3-output networks).
-__device__ inline int index_to_code(int idx) { return idx == 0 ? 1 : (idx == 1 ? 2 : 0); }
+__device__ inline int index_to_code(int idx) {  // 0 -> 1, 1 -> 2, 2, 3 -> 0: bits 2 idx of 0b1001
+  return (int)__builtin_amdgcn_ubfe(9u, 2u * (unsigned)idx, 2u);
+}
 
 // ---- wave-level helpers ----
 template <int CTRL>

@@ -295,9 +295,10 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       const int mine = index_to_code(idx);
       const int other = other_half<L>(mine);
       right = side ? other : mine;
-      if (left_nn) {
-        left = side ? mine : other;
-      } else {  // HardcodedAi / ScoreHardcodedAi (dumb_ais.py), group-uniform: skipped in self-play
+      left = side ? mine : other;
+      // HardcodedAi / ScoreHardcodedAi (dumb_ais.py): behind a wave-uniform
+      // test, which a self-play schedule never passes
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!left_nn) != 0, 0) && !left_nn) {
         left = hardcoded(by2, lc2);
         if (kind == kOppScore && st.s1 > st.s2) left = 0;
       }

@@ -18,34 +18,65 @@ import sys
 
 # (file suffix, first line, last line, phase) -- ranges of the sources; the
 # first match wins.  "rare" ranges are skipped when a branch jumps over them.
-PHASES = [  # pg_service.hpp line ranges of round 3's k_service (adjust after edits)
-    ("pg_service.hpp", 161, 186, "rare:start"),
-    ("pg_service.hpp", 194, 203, "hidden-jump gate"),
-    ("pg_service.hpp", 204, 215, "rare:hidden-jump"),
-    ("pg_service.hpp", 246, 294, "rare:cert-fail"),
-    ("pg_service.hpp", 308, 313, "rare:trace"),
-    ("pg_service.hpp", 334, 335, "rally gate"),
-    ("pg_service.hpp", 336, 358, "rare:rally"),
-    ("pg_service.hpp", 360, 400, "rare:game-end"),
-    ("pg_service.hpp", 216, 228, "physics+features"),
-    ("pg_service.hpp", 229, 245, "network+certify"),
-    ("pg_service.hpp", 295, 307, "decision-exchange+clamp"),
-    ("pg_service.hpp", 314, 319, "no-score counter"),
-    ("pg_service.hpp", 359, 359, "termination test"),
-    ("pg_service.hpp", 150, 160, "loop"),
-    ("pg_device.hpp", 144, 155, "rare:serve"),
-    ("pg_device.hpp", 102, 120, "rare:face"),
-    ("pg_device.hpp", 133, 143, "rare:hidden-jump"),
-    ("pg_device.hpp", 56, 132, "physics+features"),
-    ("pg_device.hpp", 196, 202, "physics+features"),
-    ("pg_device.hpp", 204, 217, "decision-exchange+clamp"),
-    ("pg_device.hpp", 225, 260, "network+certify"),
-    ("pg_device.hpp", 156, 195, "rare:rally"),
-    ("pg_cascade.hpp", 587, 700, "rare:cert-fail"),
-    ("pg_cascade.hpp", 800, 830, "rare:cert-fail"),
-    ("pg_cascade.hpp", 1, 2000, "network+certify"),
-    ("__clang_hip_math.h", 1, 100000, "math (fmin/fmax/exp)"),
+CSRC = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(
+    __import__("os").path.abspath(__file__))), "neuro-genetic-pong-self-play_amd", "csrc")
+
+# (file, first-line anchor, last-line anchor, phase): source ranges found by
+# the text of their first and last lines (substring match, first occurrence
+# at or after the previous anchor of the same file); the first range that
+# contains a line wins.  "rare" ranges are skipped when a branch jumps over them.
+ANCHORS = [
+    ("pg_service.hpp", "if (fresh) {  // start game w", "g_fails = g_slow = 0;", "rare:start", 2),
+    ("pg_service.hpp", "const bool hid =", "if (!kTrace && __builtin_amdgcn_ballot_w64", "hidden-jump gate"),
+    ("pg_service.hpp", "const int h = st.timer - 1;", "hidden += h;", "rare:hidden-jump"),
+    ("pg_service.hpp", "if (idx < 0) {  // rare, half-uniform", "lds_st(&slots[sx].flag, 0);", "rare:cert-fail"),
+    ("pg_service.hpp", "if (p.trace) {  // a wave-uniform test first", "(vis << 4));", "rare:trace"),
+    ("pg_service.hpp", "if (__builtin_expect(__builtin_amdgcn_ballot_w64(!left_nn)", "if (kind == kOppScore", "rare:scripted"),
+    ("pg_service.hpp", "PG_PP(pp_rally,", "if (bounced && timeout >= kRallyStart", "rally gate"),
+    ("pg_service.hpp", "const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot", "slots[rs].rally_span = 2 *", "rare:rally"),
+    ("pg_service.hpp", "if (lig == 0) finish_game(p, w, st, frames, total);", "fresh = true;", "rare:game-end"),
+    ("pg_service.hpp", "const int s1b = st.s1, s2b = st.s2;", "int left = 0, right = 0;", "physics+features"),
+    ("pg_service.hpp", "if (vis) {  // get_actions", "PG_PP(pp_fail, idx < 0);", "network+certify"),
+    ("pg_service.hpp", "const int mine = index_to_code(idx);", "act_r = clamp_action(rc2, right);", "decision-exchange+clamp"),
+    ("pg_service.hpp", "{  // calculate_timeout_and_frames", "rally_at = -1;  // the next rally", "no-score counter"),
+    ("pg_service.hpp", "if (st.s1 >= kWinScore || st.s2 >= kWinScore", "if (st.s1 >= kWinScore || st.s2 >= kWinScore", "termination test"),
+    ("pg_service.hpp", "while (w < games_total) {", "while (w < games_total) {", "loop"),
+    ("pg_device.hpp", "__device__ void serve() {", "point += 1;", "rare:serve"),
+    ("pg_device.hpp", "if (__builtin_expect(to_left || to_right", "vis = 0;", "rare:face"),
+    ("pg_device.hpp", "const int bc2 = 2 * by + kBallH - 1, pc2", "lpy = one_player ? move(", "rare:one-player"),
+    ("pg_device.hpp", "__device__ static int drift(", "return py + kPaddleSpeed", "rare:hidden-jump"),
+    ("pg_device.hpp", "__device__ inline uint64_t rally_key(", "return k;", "rare:rally"),
+    ("pg_device.hpp", "struct Pong {", "__device__ void serve() {", "physics+features"),
+    ("pg_device.hpp", "__device__ inline int paddle_c2(", "return lo + hi;", "physics+features"),
+    ("pg_device.hpp", "__device__ inline int clamp_action(", "__device__ inline int index_to_code", "decision-exchange+clamp"),
+    ("pg_device.hpp", "return (int)__builtin_amdgcn_ubfe(9u", "return (int)__builtin_amdgcn_ubfe(9u", "decision-exchange+clamp"),
+    ("pg_device.hpp", "template <int CTRL>", "__device__ __forceinline__ float group_sum", "network+certify"),
+    ("pg_device.hpp", "__device__ __forceinline__ float group_sum", "return v;", "network+certify"),
+    ("pg_cascade.hpp", "__device__ __forceinline__ int plateau_f32(", "// Plateau certificate, tried first", "rare:cert-fail"),
+    ("pg_cascade.hpp", "__device__ __forceinline__ uint64_t memo_key(", "}", "rare:cert-fail"),
+    ("pg_cascade.hpp", "struct NetP {", "__device__ __forceinline__ int plateau_f32(", "network+certify"),
 ]
+PHASES = []
+
+
+def _resolve():
+    import os
+    cache = {}
+    for f, a0, a1, ph, *extra in ANCHORS:
+        if f not in cache:
+            cache[f] = open(os.path.join(CSRC, f)).read()
+        text = cache[f]
+        i0 = text.find(a0)
+        if i0 < 0:
+            print(f"warning: anchor not found in {f}: {a0!r}", file=sys.stderr)
+            continue
+        i1 = text.find(a1, i0)
+        if i1 < 0:
+            i1 = i0
+        l0 = text.count("\n", 0, i0) + 1
+        l1 = text.count("\n", 0, i1 + len(a1)) + 1 + (extra[0] if extra else 0)
+        PHASES.append((f, l0, l1, ph))
+    PHASES.append(("__clang_hip_math.h", 1, 10 ** 6, "math (fmin/fmax/exp)"))
 
 
 def phase_of(loc):
@@ -73,6 +104,7 @@ def parse(path):
 
 
 def main(path):
+    _resolve()
     insts = parse(path)
     by_addr = {a: i for i, (a, _, _) in enumerate(insts)}
 
@@ -83,12 +115,18 @@ def main(path):
             off -= 65536
         return addr + 4 + 4 * off
 
-    # the loop head: the first instruction of the game-start block's branch
-    start = next(i for i, (_, _, l) in enumerate(insts) if l and phase_of(l) == "rare:start")
-    # back up to the branch that skips it
-    i = start
-    while not insts[i][1].startswith("s_cbranch"):
-        i -= 1
+    # the loop head: the first conditional branch that jumps over (mostly) the game-start block
+    i = None
+    for k, (addr, text, _) in enumerate(insts):
+        if not text.startswith("s_cbranch"):
+            continue
+        j = by_addr.get(target(text, addr))
+        if j is None or j <= k + 8:
+            continue
+        sk = [phase_of(l) for _, _, l in insts[k + 1:j]]
+        if sum(p == "rare:start" for p in sk) * 2 >= len(sk):
+            i = k
+            break
     counts = collections.Counter()
     kinds = collections.Counter()
     seen = 0
