@@ -14,6 +14,12 @@
 
 namespace pg {
 
+// A test every lane of the wave evaluates, taken as a wave-uniform branch: a
+// wave where no lane needs the guarded block skips it with one scalar branch
+// instead of the exec-mask save / restore of a divergent one.  Use as
+// `if (PG_ANY(c) && c) { ... }` for blocks most frames skip.
+#define PG_ANY(c) __builtin_expect(__builtin_amdgcn_ballot_w64(c) != 0, 0)
+
 // ---- playfield geometry: the 160x160 crop (rows 34..193) of obs.npy ----
 constexpr int kFieldW = 160;
 constexpr int kFieldH = 160;
@@ -90,14 +96,14 @@ struct Pong {
   // env.step(action) (main.py:77): right [up,down] = action[4:6], left = action[6:8].
   // The common case -- the ball in flight, away from both paddle faces -- is
   // straight-line code; reaching a face (bounce or miss, ~1 frame in 40 of a
-  // game) and the hidden-ball countdown are branches.  The lanes of a group
-  // play one game, so a branch only costs the waves where some game takes it.
+  // game) and the hidden-ball countdown are wave-uniform branches (PG_ANY):
+  // they cost only the waves where some game takes them.
   __device__ void step(int right_code, int left_code) {
     rpy = move_player(rpy, right_code);
     // left paddle: the action, or the built-in CPU of the 1-player env
     // (main.py:40) -- behind a wave-uniform test: no game of a self-play
     // schedule takes it
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(one_player != 0) != 0, 0)) {
+    if (PG_ANY(one_player != 0)) {
       const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
       const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
       lpy = one_player ? move(lpy, cpu_dy, kCpuSpeed) : move_player(lpy, left_code);
@@ -107,40 +113,43 @@ struct Pong {
 
     constexpr int ymax = kFieldH - kBallH;
     constexpr int lface = kLeftPaddleX + kPaddleW, rface = kRightPaddleX;
-    if (vis) {
-      // ball in play: move, walls
-      const int nx = bx + vx;
-      int ny = by + vy;
-      const bool wall_top = ny < 0, wall_bot = ny > ymax;
-      ny = wall_top ? -ny : (wall_bot ? 2 * ymax - ny : ny);
-      const int wvy = (wall_top || wall_bot) ? -vy : vy;
-      const bool to_left = (vx < 0) && (nx <= lface - 1);
-      const bool to_right = (vx > 0) && (nx + kBallW - 1 >= rface);
-      if (__builtin_expect(to_left || to_right, 0)) {  // crossing a paddle face: bounce or miss
-        const int py = to_left ? lpy : rpy;
-        if ((ny <= py + kPaddleH - 1) && (ny + kBallH - 1 >= py)) {  // rows overlap: bounce
-          hits += 1;
-          const int mag = min(kBallVx0 + (hits >> 2), kBallVxMax);
-          // (2 (ny - py) - 12) / 6 truncated toward zero; |d| <= 18 is even, so |d| / 6 == (|d| * 43) >> 8
-          const int d = 2 * (ny - py) - 12;
-          const int q = (abs(d) * 43) >> 8;
-          bx = to_left ? lface : rface - kBallW;
-          by = ny;
-          vx = to_left ? mag : -mag;
-          vy = d < 0 ? -q : q;
-        } else {  // a miss scores for the other side; the ball stays, hidden until the next serve
-          s2 += to_left ? 1 : 0;
-          s1 += to_right ? 1 : 0;
-          dir = to_left ? -1 : 1;
-          timer = kServeDelay;
-          vis = 0;
-        }
-      } else {
-        bx = nx;
+    // ball in play: move, walls; the plain flight as selects, reaching a face
+    // and the hidden ball behind wave-uniform tests (no exec-mask juggling on
+    // the frames where no game of the wave needs them)
+    const bool play = vis != 0;
+    const int nx = bx + vx;
+    int ny = by + vy;
+    const bool wall_top = ny < 0, wall_bot = ny > ymax;
+    ny = wall_top ? -ny : (wall_bot ? 2 * ymax - ny : ny);
+    const int wvy = (wall_top || wall_bot) ? -vy : vy;
+    const bool to_left = play && (vx < 0) && (nx <= lface - 1);
+    const bool to_right = play && (vx > 0) && (nx + kBallW - 1 >= rface);
+    const bool face = to_left || to_right;
+    const bool fly = play && !face;
+    bx = fly ? nx : bx;
+    by = fly ? ny : by;
+    vy = fly ? wvy : vy;
+    if (PG_ANY(face) && face) {  // crossing a paddle face: bounce or miss
+      const int py = to_left ? lpy : rpy;
+      if ((ny <= py + kPaddleH - 1) && (ny + kBallH - 1 >= py)) {  // rows overlap: bounce
+        hits += 1;
+        const int mag = min(kBallVx0 + (hits >> 2), kBallVxMax);
+        // (2 (ny - py) - 12) / 6 truncated toward zero; |d| <= 18 is even, so |d| / 6 == (|d| * 43) >> 8
+        const int d = 2 * (ny - py) - 12;
+        const int q = (abs(d) * 43) >> 8;
+        bx = to_left ? lface : rface - kBallW;
         by = ny;
-        vy = wvy;
+        vx = to_left ? mag : -mag;
+        vy = d < 0 ? -q : q;
+      } else {  // a miss scores for the other side; the ball stays, hidden until the next serve
+        s2 += to_left ? 1 : 0;
+        s1 += to_right ? 1 : 0;
+        dir = to_left ? -1 : 1;
+        timer = kServeDelay;
+        vis = 0;
       }
-    } else {
+    }
+    if (PG_ANY(!play) && !play) {
       // ball hidden: the serve timer runs down (the frame of a miss only starts it)
       timer = timer > 0 ? timer - 1 : 0;
       if (timer == 0 && !done()) serve();

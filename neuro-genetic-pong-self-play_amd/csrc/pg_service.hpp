@@ -243,7 +243,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       if (idx < 0) idx = z[1] > z[0] ? 1 : 0;
 #endif
       PG_PP(pp_fail, idx < 0);
-      if (idx < 0) {  // rare, half-uniform: the memo, else ask the service wave
+      if (PG_ANY(idx < 0) && idx < 0) {  // rare, half-uniform: the memo, else ask the service wave
         fails += 1;
 #ifdef PG_TIMELINE
         g_fails += 1;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         idx = plateau_f32<O>(z, net.e);
         inwave += idx >= 0 ? 1 : 0;
       }
-      if (idx < 0) {
+      if (PG_ANY(idx < 0) && idx < 0) {
         const uint64_t key = memo_key(k);
         const int nm = slots[sx].n_memo;
         int hit = -1;
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       const bool same = st.s1 + st.s2 == s1b + s2b;
       total += same ? 0 : timeout;
       timeout = same ? timeout + 1 : 0;
-      if (!same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
+      if (PG_ANY(!same) && !same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
     }
 #ifndef PG_NO_RALLY_SKIP
     // a periodic rally ends at the timeout with nothing else changed: jump there
@@ -335,7 +335,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // kRallyStride frames: 15 % -> 2 % of wave-frames build a key
     // (profiles/r03/sweep_frame_trims_g5.log).
     PG_PP(pp_rally, bounced && timeout >= kRallyStart && timeout <= kTimeoutThresh);
-    if (bounced && timeout >= kRallyStart && timeout <= kTimeoutThresh && !kTracing) {
+    if (!kTracing && PG_ANY(bounced && timeout >= kRallyStart && timeout <= kTimeoutThresh) && bounced &&
+        timeout >= kRallyStart && timeout <= kTimeoutThresh) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
       const uint64_t key = rally_key(st, act_r, act_l);
       const int at = slots[rs].rally_at;
@@ -359,7 +360,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       }
     }
 #endif
-    if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
+    const bool over = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh;
+    if (PG_ANY(over) && over) {
       if (lig == 0) finish_game(p, w, st, frames, total);
 #ifdef PG_TIMELINE
       if (p.trace && w < p.trace_games && lig == 0) {

@@ -6,7 +6,10 @@ conditional branch whose skipped range is mostly RARE source lines (game
 start, serve, hidden-ball jump, certificate failure paths, rally check, game
 end, tracing), and counts the instructions met per phase until the loop's
 back edge.  A static model: no latencies, the common case only (ball visible
-in every game of the wave, no face crossing, every certificate passing).
+in every game of the wave, no face crossing, every certificate passing); the
+walk assumes rare blocks lie between a branch and its target, so a layout that
+moves them out of line (wave-uniform branches) can end it early -- compare
+builds with the GPU A/B, not with this count alone.
 
     hipcc ... -gline-tables-only --cuda-device-only --no-gpu-bundle-output -c -o k.o pong_ga.hip
     llvm-objdump -d -l --no-show-raw-insn --disassemble-symbols=SYM k.o > k.s
@@ -29,20 +32,21 @@ ANCHORS = [
     ("pg_service.hpp", "if (fresh) {  // start game w", "g_fails = g_slow = 0;", "rare:start", 2),
     ("pg_service.hpp", "const bool hid =", "if (!kTrace && __builtin_amdgcn_ballot_w64", "hidden-jump gate"),
     ("pg_service.hpp", "const int h = st.timer - 1;", "hidden += h;", "rare:hidden-jump"),
-    ("pg_service.hpp", "if (idx < 0) {  // rare, half-uniform", "lds_st(&slots[sx].flag, 0);", "rare:cert-fail"),
+    ("pg_service.hpp", "if (PG_ANY(idx < 0) && idx < 0) {  // rare", "lds_st(&slots[sx].flag, 0);", "rare:cert-fail"),
     ("pg_service.hpp", "if (p.trace) {  // a wave-uniform test first", "(vis << 4));", "rare:trace"),
     ("pg_service.hpp", "if (__builtin_expect(__builtin_amdgcn_ballot_w64(!left_nn)", "if (kind == kOppScore", "rare:scripted"),
-    ("pg_service.hpp", "PG_PP(pp_rally,", "if (bounced && timeout >= kRallyStart", "rally gate"),
+    ("pg_service.hpp", "PG_PP(pp_rally,", "timeout >= kRallyStart && timeout <= kTimeoutThresh) {", "rally gate"),
     ("pg_service.hpp", "const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot", "slots[rs].rally_span = 2 *", "rare:rally"),
     ("pg_service.hpp", "if (lig == 0) finish_game(p, w, st, frames, total);", "fresh = true;", "rare:game-end"),
     ("pg_service.hpp", "const int s1b = st.s1, s2b = st.s2;", "int left = 0, right = 0;", "physics+features"),
     ("pg_service.hpp", "if (vis) {  // get_actions", "PG_PP(pp_fail, idx < 0);", "network+certify"),
     ("pg_service.hpp", "const int mine = index_to_code(idx);", "act_r = clamp_action(rc2, right);", "decision-exchange+clamp"),
     ("pg_service.hpp", "{  // calculate_timeout_and_frames", "rally_at = -1;  // the next rally", "no-score counter"),
-    ("pg_service.hpp", "if (st.s1 >= kWinScore || st.s2 >= kWinScore", "if (st.s1 >= kWinScore || st.s2 >= kWinScore", "termination test"),
+    ("pg_service.hpp", "const bool over = st.s1 >= kWinScore", "if (PG_ANY(over) && over) {", "termination test"),
     ("pg_service.hpp", "while (w < games_total) {", "while (w < games_total) {", "loop"),
     ("pg_device.hpp", "__device__ void serve() {", "point += 1;", "rare:serve"),
-    ("pg_device.hpp", "if (__builtin_expect(to_left || to_right", "vis = 0;", "rare:face"),
+    ("pg_device.hpp", "if (PG_ANY(face) && face) {", "vis = 0;", "rare:face"),
+    ("pg_device.hpp", "if (PG_ANY(!play) && !play) {", "if (timer == 0 && !done()) serve();", "rare:hidden-countdown"),
     ("pg_device.hpp", "const int bc2 = 2 * by + kBallH - 1, pc2", "lpy = one_player ? move(", "rare:one-player"),
     ("pg_device.hpp", "__device__ static int drift(", "return py + kPaddleSpeed", "rare:hidden-jump"),
     ("pg_device.hpp", "__device__ inline uint64_t rally_key(", "return k;", "rare:rally"),
@@ -127,6 +131,17 @@ def main(path):
         if sum(p == "rare:start" for p in sk) * 2 >= len(sk):
             i = k
             break
+    def rareness(x):
+        n = r = 0
+        while x < len(insts) and n < 40:
+            t = insts[x][1]
+            if t.startswith(("s_cbranch", "s_branch")):
+                break
+            n += 1
+            r += phase_of(insts[x][2]).startswith("rare")
+            x += 1
+        return r / n if n else 0.0
+
     counts = collections.Counter()
     kinds = collections.Counter()
     seen = 0
