@@ -54,19 +54,34 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   constexpr int kSlots = kSvcGameWaves * (64 / L) * 2;
   __shared__ SlowSlot slots[kSlots];
   __shared__ int waves_done;
+  __shared__ int posted;  // requests posted so far (the service wave polls this one word)
   extern __shared__ double lds_svc[];  // f64_lds_doubles(H, O), service wave only
   const int H = p.nodes[1];
   const int b = p.bias;
   const int wave = threadIdx.x >> 6;
   const int lane64 = threadIdx.x & 63;
   for (int i = threadIdx.x; i < kSlots; i += kSvcThreads) lds_st(&slots[i].flag, 0);
-  if (threadIdx.x == 0) lds_st(&waves_done, 0);
+  if (threadIdx.x == 0) {
+    lds_st(&waves_done, 0);
+    lds_st(&posted, 0);
+  }
   __syncthreads();
 
   if (wave == kSvcGameWaves) {
     // ---------------- service wave: f64 re-decisions for the whole block ----
+    // An idle poll reads one word (the posted count): the slot scan runs only
+    // when it moved.  A request posted after the read moves it again, so the
+    // next poll scans once more; the poster's flag store is ordered before
+    // its count increment (LDS operations of a wave complete in order).
+    int seen = 0;
     for (;;) {
-      bool served = false;
+      const int now = __builtin_amdgcn_readfirstlane(lds_ld(&posted));
+      if (now == seen) {
+        if (lds_ld(&waves_done) == kSvcGameWaves) break;
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      seen = now;
       for (int base = 0; base < kSlots; base += 64) {
         const int sidx = base + lane64;
         const bool posted = sidx < kSlots && lds_ld(&slots[sidx].flag) == 1;
@@ -102,12 +117,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
             __threadfence_block();
             lds_st(&slots[sl].flag, 2);
           }
-          served = true;
         }
-      }
-      if (!served) {
-        if (lds_ld(&waves_done) == kSvcGameWaves) break;
-        __builtin_amdgcn_s_sleep(2);
       }
     }
     return;
@@ -273,6 +283,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
             slots[sx].e = net.e;
             __threadfence_block();
             lds_st(&slots[sx].flag, 1);
+            __hip_atomic_fetch_add(&posted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
           while (lds_ld(&slots[sx].flag) != 2) __builtin_amdgcn_s_sleep(1);
           __threadfence_block();

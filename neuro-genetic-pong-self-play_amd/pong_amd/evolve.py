@@ -498,11 +498,12 @@ class DeviceGA:
         packed_h.copy_(packed, non_blocking=True)
         copied = torch.cuda.Event()
         copied.record()
+        self._mark("hof_prepare", sub=True)  # (profiling only: these marks synchronise)
         if overlap:
             overlap()
+            self._mark("next_select_vary", sub=True)
         copied.synchronize()
         pk = packed_h.numpy()
-        self._mark("hof_prepare", sub=True)
         rank_np = (pk[:n] & 0xFFFFFFFF).astype(np.int32)
         cls_np = pk[:n] >> 32
         src, new_fit = D.hof_update(self.H, self._hof_fit_host, cls_np[:old_n], pk[n:].view(np.float64),
