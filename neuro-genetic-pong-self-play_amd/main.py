@@ -5,7 +5,10 @@ GAMES_TO_PLAY games, as a 1-tuple); ``evaluate_population(individuals)`` is
 the same computation for a whole batch in one device launch
 (pg_eval_population), and ``toolbox.map`` routes eaSimple's
 ``map(evaluate, invalid_ind)`` there.  ``main()`` is the reference's endless
-eaSimple + checkpoint loop.  Rendering and human play are out of scope.
+eaSimple + checkpoint loop.  ``perform_episode(env, left_model, right_model,
+render, score_multiplier)`` plays one game in one launch on a ``DeviceEnv``
+(``make_env``); ``get_actions`` is the per-frame decision through the
+drop-in models.  A viewer window and human play are out of scope.
 """
 import numpy as np
 import torch
@@ -19,6 +22,7 @@ import ga
 import utils
 from config import *  # noqa: F401,F403
 from ga import hall_of_fame, toolbox
+from pong_amd import _lib as L
 from pong_amd import runtime, schedule
 from utils import pick_hall_of_famer, save_checkpoint
 
@@ -89,6 +93,106 @@ def _evaluate_rendered(individual):
 
 
 evaluate.__pong_batch__ = evaluate_population
+
+
+class DeviceEnv:
+    """The env ``perform_episode`` plays (the retro env of main.py:35-55): one
+    game of the build's Pong -- the emulator is absent --
+    in game slot ``game`` (the slot fixes the game's serves, as
+    ``evaluate``'s i-th game does), two players, or ``players=1`` for the
+    1-player env whose left paddle is the built-in CPU (main.py:39-40)."""
+
+    def __init__(self, game=0, players=2):
+        self.game, self.players = int(game), int(players)
+        self.use_restricted_actions = None
+
+    def reset(self):
+        pass
+
+    def close(self):
+        pass
+
+
+def make_env(game=0, players=2):
+    return DeviceEnv(game, players)
+
+
+_SLOT_MUL = 0xA24BAED4963EE407  # game_seed's slot multiplier (pg_device.hpp)
+
+
+def _slot_seed(game):
+    # game_seed(base, g) = splitmix64(base ^ M (g + 1)): a one-game launch (slot
+    # 0) plays slot ``game`` of PHYSICS_SEED from the base PHYSICS_SEED ^ M (game + 1) ^ M
+    m = (1 << 64) - 1
+    return (PHYSICS_SEED ^ ((_SLOT_MUL * (game + 1)) & m) ^ _SLOT_MUL) & m  # noqa: F405
+
+
+def perform_episode(env, left_model, right_model, render=False, score_multiplier=1):
+    """One game to its end (main.py:69-112), played by the device in one
+    launch (pg_eval_population, one genome, one game): returns the right
+    player's reward, 0 on a drawn score, as perform_episode does.
+
+    ``right_model`` is a ``numpy_nn.NeuralNetwork``; ``left_model`` a
+    NeuralNetwork (self-play / hall-of-fame game, ``score_multiplier`` scales
+    the reward, main.py:47-49), a ``HardcodedAi`` or a ``ScoreHardcodedAi``;
+    on a 1-player ``env`` the left model is ignored, as the reference's
+    emulator ignores the second player's buttons.  ``render`` writes the game
+    as a GIF under REPLAY_DIR (no viewer window).
+    """
+    from dumb_ais import HardcodedAi, ScoreHardcodedAi
+    from numpy_nn import NeuralNetwork
+    if not isinstance(right_model, NeuralNetwork):
+        raise TypeError("right_model must be a numpy_nn.NeuralNetwork")
+    opponents = None
+    if getattr(env, "players", 2) == 1:
+        kind = L.PG_OPP_ROM_CPU
+    elif isinstance(left_model, NeuralNetwork):
+        kind, opponents = L.PG_OPP_NN, left_model._genes
+    elif isinstance(left_model, ScoreHardcodedAi):
+        kind = L.PG_OPP_SCORE
+    elif isinstance(left_model, HardcodedAi):
+        kind = L.PG_OPP_HARDCODED
+    else:
+        raise TypeError(f"left_model {type(left_model).__name__} has no device game kind")
+    ev = runtime.evaluator(right_model.nodes, bool(right_model.bias), 1, "float64", PRECISION,  # noqa: F405
+                           _slot_seed(getattr(env, "game", 0)), DEVICE)  # noqa: F405
+    dev = ev.device
+    kind_t = torch.tensor([[kind]], dtype=torch.int32, device=dev)
+    opp_t = torch.zeros((1, 1), dtype=torch.int32, device=dev)
+    mult_t = torch.tensor([[float(score_multiplier)]], dtype=torch.float64, device=dev)
+    if render:
+        import os
+
+        from pong_amd import replay
+        res, frames = replay.replay(ev, right_model._genes[0], kind_t[0].cpu().numpy(), opp_t[0].cpu().numpy(),
+                                    mult_t[0].cpu().numpy(), opponents=opponents)
+        if len(frames[0]):
+            replay.write_gif(frames[0], os.path.join(REPLAY_DIR, f"episode_{getattr(env, 'game', 0)}.gif"),  # noqa: F405
+                             fps=FPS)  # noqa: F405
+    else:
+        res, _ = ev.evaluate(right_model._genes, kind_t, opp_t, mult_t, opponents=opponents)
+    if int(res.status[0]):  # calculate_reward with total_frames == 0 (utils.py:106-108)
+        raise ZeroDivisionError("float division by zero")
+    return float(res.rewards[0, 0])
+
+
+def get_actions(ball_location, last_ball_location, left_location, left_model, right_location, right_model):
+    """The two paddles' [up, down] for one frame (main.py:138-154): a visible
+    ball and a visible paddle decide through the model (the left player sees
+    the field x-flipped); a missing paddle keeps a random action; no ball, no
+    move.  Each model call is one device forward (numpy_nn.NeuralNetwork.run)."""
+    if ball_location is None:
+        return [0, 0], [0, 0]
+    last = ball_location if last_ball_location is None else last_ball_location
+    left_action = utils.get_random_action(ALL_ACTIONS)  # noqa: F405
+    right_action = utils.get_random_action(ALL_ACTIONS)  # noqa: F405
+    if left_location is not None:
+        def flip(loc):  # [row, column] with the column mirrored
+            return [loc[0], GAME_WIDTH - loc[1]]  # noqa: F405
+        left_action = utils.inference(flip(ball_location), flip(last), left_location, right_location, left_model)
+    if right_location is not None:
+        right_action = utils.inference(ball_location, last, right_location, left_location, right_model)
+    return left_action, right_action
 
 
 def calculate_timeout_and_frames(last_score, score_info, timeout_counter, total_frames):

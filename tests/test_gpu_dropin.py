@@ -153,3 +153,48 @@ def test_main_block_checkpoint_reference_readable(gpu, tmp_path, monkeypatch):
     assert got["genes"] == [list(i) for i in pop]
     assert got["fit"] == [i.fitness.values[0] for i in pop]
     assert got["hof"] == [i.fitness.values[0] for i in hof.items]
+
+
+def test_perform_episode_and_get_actions(gpu, oracle):
+    """perform_episode (main.py:69-112) on the drop-in: each opponent kind in
+    its evaluate() slot equals the oracle's game of the same slot (reward
+    bit for bit, the hall-of-fame multiplier included) and evaluate()'s own
+    game; get_actions (main.py:138-154) decides as the oracle's forward on the
+    x-flipped left view and the right view."""
+    import main
+    import utils
+    from dumb_ais import HardcodedAi, ScoreHardcodedAi
+    from numpy_nn import NeuralNetwork
+    shape = [6, 64, 3]
+    saved = utils.NETWORK_SHAPE
+    utils.NETWORK_SHAPE = shape
+    try:
+        rng = np.random.default_rng(31)
+        G = sum((shape[i] + 1) * shape[i + 1] for i in range(len(shape) - 1))
+        me, other = rng.standard_normal(G) * 3.0, rng.standard_normal(G) * 3.0
+        right = NeuralNetwork(nodes=shape, weights=list(me), bias=True)
+        left = NeuralNetwork(nodes=shape, weights=list(other), bias=True)
+        cases = [(0, 2, HardcodedAi(), 1.0, 0), (1, 1, HardcodedAi(), 1.0, 1), (2, 2, ScoreHardcodedAi(), 1.0, 2),
+                 (4, 2, left, -0.375, 3)]
+        for game, players, lm, mult, kind in cases:
+            got = main.perform_episode(main.make_env(game, players), lm, right, False, mult)
+            ref = oracle.play_game(me, shape, kind, other if kind == 3 else None, mult,
+                                   seed=oracle.game_seed(main.PHYSICS_SEED, game))
+            assert got == ref["reward"], (game, got, ref)
+        # get_actions: [row, column] locations (find_stuff's order), doubled-centroid grid points
+        for _ in range(40):
+            ball = [float(rng.integers(0, 160)), float(rng.integers(0, 160))]
+            last = [float(rng.integers(0, 160)), float(rng.integers(0, 160))]
+            lpad, rpad = [float(rng.integers(8, 152)), 17.5], [float(rng.integers(8, 152)), 141.5]
+            la, ra = main.get_actions(ball, last, lpad, left, rpad, right)
+            # the oracle's forward on the features utils.inference builds (the left view x-flipped)
+            W, Hh = utils.GAME_WIDTH, utils.GAME_PLAYABLE_HEIGHT
+            for act, net_genes, b, lb, mine, enemy in ((la, other, [ball[0], W - ball[1]], [last[0], W - last[1]],
+                                                        lpad, rpad),
+                                                       (ra, me, ball, last, rpad, lpad)):
+                feats = [b[1] / W, b[0] / Hh, lb[1] / W, lb[0] / Hh, mine[0] / Hh, enemy[0] / Hh]
+                idx, _ = oracle.nn_run(net_genes, shape, np.array(feats))
+                assert list(act) == ([1, 0] if idx == 0 else [0, 1] if idx == 1 else [0, 0])
+        assert main.get_actions(None, None, [80.0, 17.5], left, [80.0, 141.5], right) == ([0, 0], [0, 0])
+    finally:
+        utils.NETWORK_SHAPE = saved
