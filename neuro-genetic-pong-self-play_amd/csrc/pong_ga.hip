@@ -618,13 +618,29 @@ __global__ __launch_bounds__(256) void k_vary(pg_ga_args a) {
     o1[gene] = (WT)x1;
     if (has1) o2[gene] = (WT)x2;
   };
-  for (long g0 = 0; g0 < a.genes; g0 += 128) {
-    const long ga = g0 + lane, gb = g0 + 64 + lane;
-    const bool va = ga < a.genes, vb = gb < a.genes;
-    const double a1 = va ? (double)p1[ga] : 0.0, a2 = va && has1 ? (double)p2[ga] : 0.0;
-    const double b1 = vb ? (double)p1[gb] : 0.0, b2 = vb && has1 ? (double)p2[gb] : 0.0;
-    if (va) one(ga, a1, a2);
-    if (vb) one(gb, b1, b2);
+  // kVaryChunk 128-gene pieces of both parents requested before any arithmetic
+  // (a [6,64,3] genome, 454 genes, is one chunk): more loads in flight per wave
+  constexpr int kVaryChunk = 4;
+  for (long g0 = 0; g0 < a.genes; g0 += 128 * kVaryChunk) {
+    double x[kVaryChunk][2][2];
+#pragma unroll
+    for (int c = 0; c < kVaryChunk; ++c) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const long g = g0 + c * 128 + h * 64 + lane;
+        const bool v = g < a.genes;
+        x[c][h][0] = v ? (double)p1[g] : 0.0;
+        x[c][h][1] = v && has1 ? (double)p2[g] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kVaryChunk; ++c) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const long g = g0 + c * 128 + h * 64 + lane;
+        if (g < a.genes) one(g, x[c][h][0], x[c][h][1]);
+      }
+    }
   }
   if (lane == 0) {
     a.invalid[i0] = (uint8_t)(cx || mut0);
