@@ -207,10 +207,11 @@ __device__ inline uint64_t rally_key(const Pong &s, int act_r, int act_l) {
   return k;
 }
 // Brent's cycle search over one point: the key is saved when the no-score
-// counter reaches kRallyStart and re-saved each time the distance doubles.
-// k_wide compares keys every kRallyStride frames (a multiple of the period is
-// then still met within kRallyStride periods); k_service at the frames where
-// a paddle returns the ball (pg_service.hpp).
+// counter reaches kRallyStart (k_wide) or at the point's kRallyHits-th return
+// (k_service) and re-saved each time the distance doubles.  k_wide compares
+// keys every kRallyStride frames (a multiple of the period is then still met
+// within kRallyStride periods); k_service at the frames where a paddle
+// returns the ball (pg_service.hpp).
 #ifndef PG_RALLY_START
 #define PG_RALLY_START 256
 #endif
@@ -219,6 +220,14 @@ __device__ inline uint64_t rally_key(const Pong &s, int act_r, int act_l) {
 #endif
 constexpr int kRallyStart = PG_RALLY_START;
 constexpr int kRallyStride = PG_RALLY_STRIDE;
+// k_service: the search opens at a point's kRallyHits-th return (the first
+// bounce whose state can recur: rally_key caps hits there) with a first span
+// of kRallySpan0 frames
+#ifndef PG_RALLY_SPAN0
+#define PG_RALLY_SPAN0 64
+#endif
+constexpr int kRallyHits = 8;
+constexpr int kRallySpan0 = PG_RALLY_SPAN0;
 
 // Doubled centroid row of a paddle clipped to rows [0,160): what
 // get_rect_quickly (utils.py:60-68) returns for the rendered rectangle, x2.

@@ -338,16 +338,20 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     const bool kTracing = p.trace != nullptr;
 #endif
     // Brent's cycle search sampled at the frames where a paddle returned the
-    // ball (the states at the bounces of a periodic rally repeat too): the
-    // first bounce past kRallyStart opens the rally's search (a point or a
-    // game start clears the save), a later bounce state equal to the saved one
-    // proves the rally periodic, and the save moves forward when the distance
-    // reaches the span, which doubles.  Sampling at bounces instead of every
-    // kRallyStride frames: 15 % -> 2 % of wave-frames build a key
-    // (profiles/r03/sweep_frame_trims_g5.log).
-    PG_PP(pp_rally, bounced && timeout >= kRallyStart && timeout <= kTimeoutThresh);
-    if (!kTracing && PG_ANY(bounced && timeout >= kRallyStart && timeout <= kTimeoutThresh) && bounced &&
-        timeout >= kRallyStart && timeout <= kTimeoutThresh) {
+    // ball (the states at the bounces of a periodic rally repeat too).  The key
+    // holds min(hits, 8) and hits grows by one per bounce within a point, so no
+    // state of a point repeats before its 8th return: that bounce opens the
+    // search (a point or a game start clears the save), a later bounce state
+    // equal to the saved one proves the rally periodic, and the save moves
+    // forward when the distance reaches the span (kRallySpan0 frames,
+    // doubling).  Sampling at bounces instead of every kRallyStride frames:
+    // 15 % -> 2 % of wave-frames build a key (profiles/r03/sweep_frame_trims_g5.log);
+    // opening at the 8th return instead of at timeout 256, with a 64-frame
+    // first span, fires at the cycle's first repetition in the common
+    // two-bounce rally (tools/long_games.py: 460 instead of 610 frames).
+    const bool rally_check = bounced && st.hits >= kRallyHits && timeout <= kTimeoutThresh;
+    PG_PP(pp_rally, rally_check);
+    if (!kTracing && PG_ANY(rally_check) && rally_check) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
       const uint64_t key = rally_key(st, act_r, act_l);
       const int at = slots[rs].rally_at;
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         if (lig == 0) {
           slots[rs].rally_key = key;
           slots[rs].rally_at = timeout;
-          slots[rs].rally_span = kRallyStart;
+          slots[rs].rally_span = kRallySpan0;
         }
       } else if (slots[rs].rally_key == key) {
         const int rest = kTimeoutThresh + 1 - timeout;

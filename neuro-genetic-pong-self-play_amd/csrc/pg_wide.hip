@@ -273,6 +273,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       kind = probe ? kOppHard : p.kind[w];
       orow[lane] = kind == kOppNN ? (long long)p.opp[w] * p.ostride : 0;
       st.reset(game_seed(p.seed, lane), kind == kOppRomCpu);
+      rat[lane] = -1;  // no rally search open
       active = true;
     }
     if (wid == 0) {
@@ -715,23 +716,25 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           } else {
             total += timeout;
             timeout = 0;
+            rat[lane] = -1;  // a point: the next rally searches afresh
           }
         }
 #ifndef PG_NO_RALLY_SKIP
-        // a periodic rally ends at the timeout with nothing else changed (pg_device.hpp rally_key)
-        if (timeout >= kRallyStart && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
-        !p.trace) {
+        // a periodic rally ends at the timeout with nothing else changed (pg_device.hpp
+        // rally_key); no state of a point recurs before its kRallyHits-th return
+        if (st.hits >= kRallyHits && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
+            !p.trace) {
           const uint64_t key = rally_key(st, act_r, act_l);
-          if (timeout == kRallyStart) {
+          if (rat[lane] < 0) {
             rkey[lane] = key;
             rat[lane] = timeout;
-            rspan[lane] = kRallyStart;
+            rspan[lane] = kRallySpan0;
           } else if (rkey[lane] == key) {
             const int rest = kTimeoutThresh + 1 - timeout;
             frames += rest;
             c_skip += rest;
             timeout = kTimeoutThresh + 1;
-          } else if (timeout - rat[lane] == rspan[lane]) {
+          } else if (timeout - rat[lane] >= rspan[lane]) {
             rkey[lane] = key;
             rat[lane] = timeout;
             rspan[lane] *= 2;

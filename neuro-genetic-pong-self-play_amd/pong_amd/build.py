@@ -38,6 +38,8 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    if os.environ.get("PONG_GA_LIB") and not force:
+        return LIB_PATH  # a prebuilt variant (tools/build_variant.py): never rebuilt from the product sources
     if not force and not needs_build():
         return LIB_PATH
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off"] + (
