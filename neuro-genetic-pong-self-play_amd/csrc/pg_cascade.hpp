@@ -150,6 +150,22 @@ __device__ __forceinline__ void partial_f32(const Net<U, O> &n, const float x[6]
 // over exact inputs stays within the 11u R_j hidden-error term of load_net.
 typedef float float2v __attribute__((ext_vector_type(2)));
 
+// certify()'s per-network constants, made once per game from the bound e
+// (make_cert) instead of every frame: the moved thresholds, the low-z limit,
+// the gap rule's 2e plus the plateau width's constant part, and the exponent
+// offset of its e^(top1 + e) part: 2^-50 (e^(top1+e) + 1) = 2^(top1 log2 e +
+// ee) + 2^-50 with ee = e log2 e - 50 (the f32 roundings of these forms are
+// ~1e-6 relative, inside the width's x4 margin and the bound's x2 slack).
+struct Cert {
+  float tlo, thi, lowz, e2, ee;
+};
+constexpr float kCertTlo = 36.7367f, kCertThi = 36.7369f, kCertLowZ = -708.0f;
+
+__device__ __forceinline__ Cert make_cert(float e) {
+  return Cert{kCertTlo - e, kCertThi + e, kCertLowZ + e, 2.f * e + 8.8817842e-16f,
+              e * 1.4426950408889634f - 50.f};
+}
+
 template <int U, int O>
 struct NetP {
   static constexpr int P = (U + 1) / 2;  // unit pairs
@@ -157,6 +173,7 @@ struct NetP {
   float2v w2[P][O];  // output weights of the pair
   float c[O];        // output biases
   float e;           // certified bound, as Net::e
+  Cert ct;           // certify_c's constants from e (load_rec)
 };
 
 // Number of f32 roundings in one output sum of the packed forward: a chain of
@@ -310,6 +327,7 @@ __device__ __forceinline__ void load_rec(NetP<U, O> &n, const float *__restrict_
 #pragma unroll
   for (int o = 0; o < O; ++o) n.c[o] = v[P * 14 + P * O * 2 + o];
   n.e = v[P * 14 + P * O * 2 + O];
+  n.ct = make_cert(n.e);
 }
 
 // Hidden layer and the lane-partial output sums of one packed network; k are
@@ -359,6 +377,35 @@ __device__ __forceinline__ void partial_pk(const NetP<U, O> &n, const int k[6], 
 // below that S rounds onto plateaus no wider than 2^-52 (e^z + 1) in z (x4
 // margin below).  Returns -1 when the bound cannot prove the f64 decision;
 // the caller then recomputes the forward pass in f64.
+// certify() on the per-network constants (same rule; k_service's frame)
+template <int O>
+__device__ __forceinline__ int certify_c(const float z[O], const Cert &c) {
+  int sat_res = z[O - 1] > c.thi ? O - 1 : -1;
+#pragma unroll
+  for (int o = O - 2; o >= 0; --o) sat_res = z[o] > c.thi ? o : (z[o] >= c.tlo ? -1 : sat_res);
+  float top1, top2;
+  int w;
+  if constexpr (O == 3) {
+    top1 = fmaxf(fmaxf(z[0], z[1]), z[2]);
+    top2 = __builtin_amdgcn_fmed3f(z[0], z[1], z[2]);
+    w = z[0] == top1 ? 0 : (z[1] == top1 ? 1 : 2);
+  } else {
+    top1 = z[0];
+    top2 = -3.0e38f;
+    w = 0;
+#pragma unroll
+    for (int o = 1; o < O; ++o) {
+      const bool gt = z[o] > top1;
+      top2 = gt ? top1 : fmaxf(top2, z[o]);
+      w = gt ? o : w;
+      top1 = gt ? z[o] : top1;
+    }
+  }
+  const float tw = __builtin_amdgcn_exp2f(__builtin_fmaf(top1, 1.4426950408889634f, c.ee));
+  const int uns_res = (top1 - top2 > c.e2 + tw && top1 > c.lowz) ? w : -1;
+  return top1 >= c.tlo ? sat_res : uns_res;
+}
+
 template <int O>
 __device__ __forceinline__ int certify(const float z[O], float e) {
   // Branch-free: (a) the first output that may be saturated decides if it

@@ -42,6 +42,7 @@ constexpr int kWinScore = 3;          // WIN_SCORE config.py:53
 constexpr int kTimeoutThresh = 2000;  // TIMEOUT_THRESH config.py:28
 
 enum : int { kOppHard = 0, kOppRomCpu = 1, kOppScore = 2, kOppNN = 3 };
+enum : int { kStepFly = 0, kStepBounce = 1, kStepPoint = 2 };  // Pong::step's result
 
 __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -97,8 +98,12 @@ struct Pong {
   // The common case -- the ball in flight, away from both paddle faces -- is
   // straight-line code; reaching a face (bounce or miss, ~1 frame in 40 of a
   // game) and the hidden-ball countdown are wave-uniform branches (PG_ANY):
-  // they cost only the waves where some game takes them.
-  __device__ void step(int right_code, int left_code) {
+  // they cost only the waves where some game takes them.  Returns what the
+  // frame did at a face: kStepBounce (a paddle returned the ball), kStepPoint
+  // (a miss: exactly one score grew), else kStepFly -- so a caller needs no
+  // copies of hits and the scores from before the step.
+  __device__ int step(int right_code, int left_code) {
+    int ev = kStepFly;
     rpy = move_player(rpy, right_code);
     // left paddle: the action, or the built-in CPU of the 1-player env
     // (main.py:40) -- behind a wave-uniform test: no game of a self-play
@@ -141,12 +146,14 @@ struct Pong {
         by = ny;
         vx = to_left ? mag : -mag;
         vy = d < 0 ? -q : q;
+        ev = kStepBounce;
       } else {  // a miss scores for the other side; the ball stays, hidden until the next serve
         s2 += to_left ? 1 : 0;
         s1 += to_right ? 1 : 0;
         dir = to_left ? -1 : 1;
         timer = kServeDelay;
         vis = 0;
+        ev = kStepPoint;
       }
     }
     if (PG_ANY(!play) && !play) {
@@ -154,6 +161,7 @@ struct Pong {
       timer = timer > 0 ? timer - 1 : 0;
       if (timer == 0 && !done()) serve();
     }
+    return ev;
   }
 
   // Top row of a paddle after h frames of clamp-only actions: with the ball

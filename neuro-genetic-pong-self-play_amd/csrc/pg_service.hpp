@@ -46,7 +46,9 @@ __global__ __launch_bounds__(256) void k_prep_records(EvalParams p) {
   store_rec<U, O>(n, p.recs + (net * HL + hl) * F);
 }
 
-template <int L, int U, int O, typename WT>
+// kUntraced: a launch without a trace buffer (the GA's), the trace tests
+// compiled out of the frame instead of tested on p.trace every frame
+template <int L, int U, int O, typename WT, bool kUntraced = false>
 __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   constexpr int kSvcThreads = svc_threads<U>();
   constexpr int kSvcGameWaves = kSvcThreads / 64 - 1;
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifdef PG_TIMELINE
       constexpr bool kTrace = false;
 #else
-      const bool kTrace = p.trace != nullptr;
+      const bool kTrace = !kUntraced && p.trace != nullptr;
 #endif
       const bool hid = !st.vis && st.timer >= 2;
       PG_PP(pp_hidden, hid);
@@ -223,15 +225,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       }
     }
 #endif
-    const int s1b = st.s1, s2b = st.s2;
     const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
-    const int hits_b = st.hits;
 #ifdef PG_PATH_PROBE
-    const int pt_b = st.point;
+    const int pt_b = st.point, hits_b = st.hits;
 #endif
-    st.step(act_r, act_l);
-    const bool bounced = st.hits != hits_b;  // a paddle returned the ball this frame
-    PG_PP(pp_face, st.hits != hits_b || st.s1 != s1b || st.s2 != s2b || st.point != pt_b);
+    const int ev = st.step(act_r, act_l);
+    const bool bounced = ev == kStepBounce;  // a paddle returned the ball this frame
+    PG_PP(pp_face, ev != kStepFly || st.hits != hits_b || st.point != pt_b);
     frames += 1;
     const int vis = st.vis;
     const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       partial_pk<U, O>(net, k, acc);
 #pragma unroll
       for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
-      int idx = certify<O>(z, net.e);
+      int idx = certify_c<O>(z, net.ct);
       const bool left_nn = kind == kOppNN;
       if (side && !left_nn) idx = 0;  // the left half is idle against a scripted opponent
 #ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
@@ -318,13 +318,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     act_l = clamp_action(lc2, left);
     act_r = clamp_action(rc2, right);
 #ifndef PG_TIMELINE
-    if (p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
+    if (!kUntraced && p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
       if (w < p.trace_games && frames <= p.trace_cap && lig == 0)
         p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
     }
 #endif
     {  // calculate_timeout_and_frames (main.py:128-135); at most one point a frame
-      const bool same = st.s1 + st.s2 == s1b + s2b;
+      const bool same = ev != kStepPoint;  // a miss grows exactly one score
       total += same ? 0 : timeout;
       timeout = same ? timeout + 1 : 0;
       if (PG_ANY(!same) && !same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifdef PG_TIMELINE
     constexpr bool kTracing = false;  // the timeline build's trace buffer holds stamps, not actions
 #else
-    const bool kTracing = p.trace != nullptr;
+    const bool kTracing = !kUntraced && p.trace != nullptr;
 #endif
     // Brent's cycle search sampled at the frames where a paddle returned the
     // ball (the states at the bounces of a periodic rally repeat too).  The key
@@ -440,7 +440,9 @@ inline size_t service_records_bytes(int n_genomes, int n_opponents, int L, int U
   return ((size_t)n_genomes + (size_t)(n_opponents > 0 ? n_opponents : 0)) * (size_t)(L / 2) * F * sizeof(float);
 }
 
-template <int L, int U, int O, typename WT>
+// kSplitTrace: instantiate the untraced frame too and launch it when p.trace
+// is null (the bench layout, pong_ga.hip; the other layouts test p.trace)
+template <int L, int U, int O, typename WT, bool kSplitTrace = false>
 inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
   constexpr int kSvcThreads = svc_threads<U>();
   constexpr int GPB = (kSvcThreads / 64 - 1) * (64 / L);  // game groups per block
@@ -452,7 +454,10 @@ inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
   if (!p.recs) return fail(PG_ERR_INVALID, "split kernel: no lane-record workspace");
   const long prep_threads = ((long)p.n_genomes + p.n_opponents) * (L / 2);
   hipLaunchKernelGGL((k_prep_records<L, U, O, WT>), dim3((unsigned)((prep_threads + 255) / 256)), dim3(256), 0, s, p);
-  hipLaunchKernelGGL((k_service<L, U, O, WT>), dim3(grid), dim3(kSvcThreads), lds, s, p);
+  if (kSplitTrace && !p.trace)
+    hipLaunchKernelGGL((k_service<L, U, O, WT, true>), dim3(grid), dim3(kSvcThreads), lds, s, p);
+  else
+    hipLaunchKernelGGL((k_service<L, U, O, WT, false>), dim3(grid), dim3(kSvcThreads), lds, s, p);
   PG_HIP(hipGetLastError());
   return PG_OK;
 }

@@ -812,7 +812,7 @@ static int32_t launch_service_any(const EvalParams &p, int L, int O, hipStream_t
 #endif
   // (only O = 3 here: the iterative scheduler's register allocator crashes
   // ROCm 7.2's compiler on the O = 2 / 4 instances, built in pg_service_more.hip)
-  if (here && O == 3) return launch_service<8, 16, 3, WT>(p, s);
+  if (here && O == 3) return launch_service<8, 16, 3, WT, true>(p, s);
 #ifdef PG_DEV_MIN  // variant builds for experiments (tools/build_variant.sh): the bench layout only
   return fail(PG_ERR_UNSUPPORTED, "no service kernel for L=%d H=%d O=%d", L, H, O);
 #else
