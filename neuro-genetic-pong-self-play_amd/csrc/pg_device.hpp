@@ -43,6 +43,9 @@ constexpr int kTimeoutThresh = 2000;  // TIMEOUT_THRESH config.py:28
 
 enum : int { kOppHard = 0, kOppRomCpu = 1, kOppScore = 2, kOppNN = 3 };
 enum : int { kStepFly = 0, kStepBounce = 1, kStepPoint = 2 };  // Pong::step's result
+// k_service's serve table: game slots and points per slot (a game serves at
+// most 41 times: done() at 21 points)
+constexpr int kServeTabSlots = 16, kServeTabPoints = 64;
 
 __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -103,6 +106,11 @@ struct Pong {
   // (a miss: exactly one score grew), else kStepFly -- so a caller needs no
   // copies of hits and the scores from before the step.
   __device__ int step(int right_code, int left_code) {
+    return step(right_code, left_code, [this](int pt) { return serve_entry(seed, pt); });
+  }
+  // the same with the serves read from a table: serve_of(point) = serve_entry(seed, point)
+  template <class ServeOf>
+  __device__ int step(int right_code, int left_code, ServeOf serve_of) {
     int ev = kStepFly;
     rpy = move_player(rpy, right_code);
     // left paddle: the action, or the built-in CPU of the 1-player env
@@ -159,7 +167,7 @@ struct Pong {
     if (PG_ANY(!play) && !play) {
       // ball hidden: the serve timer runs down (the frame of a miss only starts it)
       timer = timer > 0 ? timer - 1 : 0;
-      if (timer == 0 && !done()) serve();
+      if (timer == 0 && !done()) serve_from(serve_of(point));
     }
     return ev;
   }
@@ -175,17 +183,26 @@ struct Pong {
     return py + kPaddleSpeed * (down - up);
   }
 
-  __device__ void serve() {
-    const uint64_t r = splitmix64(seed ^ ((uint64_t)(point + 1) * 0xD1B54A32D192ED03ull));
+  // The (point + 1)-th serve of a game with physics seed s: the ball's row in
+  // bits 0-7, vy + 2 in bits 8-15.  A function of (seed, point) only, so
+  // k_service tabulates it per game slot once per launch (pg_service.hpp).
+  __host__ __device__ static uint32_t serve_entry(uint64_t s, int pt) {
+    const uint64_t r = splitmix64(s ^ ((uint64_t)(pt + 1) * 0xD1B54A32D192ED03ull));
     const int sel = (int)((r >> 32) & 3u);
+    const int row = 40 + (int)(r % 77u);
+    const int v = sel < 2 ? sel - 2 : sel - 1;  // {-2, -1, 1, 2}
+    return (uint32_t)row | ((uint32_t)(v + 2) << 8);
+  }
+  __device__ void serve_from(uint32_t e) {
     bx = 79;
-    by = 40 + (int)(r % 77u);
-    vy = sel < 2 ? sel - 2 : sel - 1;  // {-2, -1, 1, 2}
+    by = (int)(e & 255u);
+    vy = (int)(e >> 8) - 2;
     vx = dir * kBallVx0;
     hits = 0;
     vis = 1;
     point += 1;
   }
+  __device__ void serve() { serve_from(serve_entry(seed, point)); }
 };
 
 // ---- periodic rallies (DESIGN.md "Periodic rallies") ----

@@ -57,12 +57,20 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   __shared__ SlowSlot slots[kSlots];
   __shared__ int waves_done;
   __shared__ int posted;  // requests posted so far (the service wave polls this one word)
+  // every serve of every game slot (Pong::serve_entry is a function of the
+  // slot's physics seed and the point): a serve is one ds_read instead of a
+  // splitmix64 and a 64-bit remainder; launches with more slots compute them
+  __shared__ uint32_t serve_tab[kServeTabSlots * kServeTabPoints];
   extern __shared__ double lds_svc[];  // f64_lds_doubles(H, O), service wave only
   const int H = p.nodes[1];
   const int b = p.bias;
   const int wave = threadIdx.x >> 6;
   const int lane64 = threadIdx.x & 63;
   for (int i = threadIdx.x; i < kSlots; i += kSvcThreads) lds_st(&slots[i].flag, 0);
+  const bool tabbed = p.n_games <= kServeTabSlots;
+  if (tabbed)
+    for (int i = threadIdx.x; i < p.n_games * kServeTabPoints; i += kSvcThreads)
+      serve_tab[i] = Pong::serve_entry(game_seed(p.seed, i / kServeTabPoints), i % kServeTabPoints);
   if (threadIdx.x == 0) {
     lds_st(&waves_done, 0);
     lds_st(&posted, 0);
@@ -138,7 +146,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 
   NetP<U, O> net;
   Pong st;
-  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
+  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0, tab_off = 0;
   const WT *gm = genomes;
   uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0, hidden = 0;
 
@@ -182,7 +190,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       const int oj = nn ? min(max(p.opp[w], 0), p.n_opponents - 1) : 0;
       gm = nn ? opponents + (long)oj * p.ostride : gr;
       load_rec<U, O>(net, p.recs + ((nn ? (long)p.n_genomes + oj : (long)i) * HL + hl) * rec_floats<U, O>());
-      st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
+      st.reset(0, kind == kOppRomCpu);
+      if (!tabbed) st.seed = game_seed(p.seed, g);  // (a wave-uniform test)
+      tab_off = g * kServeTabPoints;
       act_r = act_l = total = frames = 0;
       timeout = -1;  // frame 1 does not count (main.py:94-96): it takes the counter to 0
       fresh = false;
@@ -229,7 +239,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifdef PG_PATH_PROBE
     const int pt_b = st.point, hits_b = st.hits;
 #endif
-    const int ev = st.step(act_r, act_l);
+    const int ev = st.step(act_r, act_l, [&](int pt) {
+      return tabbed && pt < kServeTabPoints ? serve_tab[tab_off + pt] : Pong::serve_entry(st.seed, pt);
+    });
     const bool bounced = ev == kStepBounce;  // a paddle returned the ball this frame
     PG_PP(pp_face, ev != kStepFly || st.hits != hits_b || st.point != pt_b);
     frames += 1;
