@@ -122,6 +122,7 @@ def main():
                   seed=args.seed, kernel=args.kernel)
     ga.ev.group_lanes = args.group_lanes
     ga.order_by_length = os.environ.get("PG_NO_LENGTH_ORDER") != "1"  # A/B switch for the evaluation order
+    ga.early_prep = os.environ.get("PG_NO_EARLY_PREP") != "1"  # A/B switch: schedule + genome records during the HoF scan
     G = ga.G
     ga.initialize("normal", args.sigma)
     # the first games already face a full hall of fame: H independent random

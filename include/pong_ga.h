@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 6
+#define PG_ABI_VERSION 7
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -111,6 +111,18 @@ typedef enum pg_kernel {
                               reports for it */
 } pg_kernel;
 
+/* pg_eval_args.prep: the SPLIT kernel's lane records (one per network of the
+ * launch) in two halves, so a caller can prepare the genomes' records while
+ * the opponents (the hall of fame) are still being decided.  Other kernels
+ * have no records: PG_PREP_GENOMES does nothing there, PG_PREP_REST = ALL. */
+typedef enum pg_prep {
+  PG_PREP_ALL = 0,      /* prepare every record, then play */
+  PG_PREP_GENOMES = 1,  /* only prepare the genomes' records into the workspace; no games are played */
+  PG_PREP_REST = 2      /* the genomes' records were prepared by a PG_PREP_GENOMES call with the same
+                           workspace, genomes, genome_rows, n_active and n_genomes: prepare the
+                           opponents' records, then play */
+} pg_prep;
+
 /* NETWORK_SHAPE (config.py:30-32) + BIAS (config.py:34) + genome storage type. */
 typedef struct pg_net {
   int32_t n_nodes;               /* len(NETWORK_SHAPE), >= 2 */
@@ -140,7 +152,7 @@ typedef struct pg_eval_args {
   int32_t *frames;               /* [n_genomes, n_games] env.step calls */
   double *total_frames;          /* [n_genomes, n_games] main.py:73 accumulator */
   int32_t *status;               /* [n_genomes] 1 = ZeroDivisionError in calculate_reward */
-  uint64_t *counters;            /* optional [16]: [0] env steps stepped one frame at a time, [1] NN
+  uint64_t *counters;            /* optional [16], zeroed by the call: [0] env steps stepped one frame at a time, [1] NN
                                     forwards, [2] numpy-order f64 forwards, [3] games; split kernel: [4]
                                     f32 certificate failures, [5] failures decided by the service wave's
                                     certified f64 rules, [6] failures decided in-wave by the f32 plateau
@@ -173,6 +185,7 @@ typedef struct pg_eval_args {
                                     (n_genomes is then an upper bound; results of blocks >= *n_active,
                                     and their counters, are left untouched) -- a count computed on the
                                     device needs no host round trip before the launch. */
+  int32_t prep;                  /* pg_prep (ABI 7): PG_PREP_ALL unless the records are prepared in two calls */
 } pg_eval_args;
 
 /* Trace byte: right_code | left_code << 2 | ball_visible << 4, where a code is

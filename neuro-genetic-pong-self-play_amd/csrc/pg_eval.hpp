@@ -47,6 +47,8 @@ struct EvalParams {
   int nodes[PG_MAX_NODES];
   int n_nodes, bias, max_width;
   float *recs;         // split kernel: lane records (k_prep_records), [n_genomes + n_opponents][L/2][rec_floats]
+  int prep;            // pg_prep: which records k_prep_records writes; it also zeroes the work header and
+                       // the counters when its launch precedes the games (PG_PREP_ALL / PG_PREP_REST)
   void *wide_scratch;  // k_wide: the blocks' tile-major W2 copies (workspace)
   int wide_w3_resident;  // k_wide: every network's W3 kept in LDS for the genome's games
   // k_wide probe (pg_wide_decide, n_games = 1): block i runs one frame of

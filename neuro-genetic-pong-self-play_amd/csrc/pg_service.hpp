@@ -27,10 +27,18 @@ template <int L, int U, int O, typename WT>
 __global__ __launch_bounds__(256) void k_prep_records(EvalParams p) {
   constexpr int HL = L / 2;
   constexpr int F = rec_floats<U, O>();
+  // the launch before the games: the work header and the counters start at zero
+  // (one kernel instead of a memset and a fill ahead of it in the stream)
+  if (p.prep != PG_PREP_GENOMES && blockIdx.x == 0) {
+    if (threadIdx.x < 64) p.work[threadIdx.x] = 0u;
+    if (p.counters && threadIdx.x < 16) p.counters[threadIdx.x] = 0ull;
+  }
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
-  const long net = t / HL;
+  // PG_PREP_GENOMES: records [0, n_genomes); PG_PREP_REST: [n_genomes, n_genomes + n_opponents)
+  const long net = t / HL + (p.prep == PG_PREP_REST ? p.n_genomes : 0);
   const int hl = (int)(t % HL);
-  if (net >= (long)p.n_genomes + p.n_opponents) return;  // whole groups (HL divides 64)
+  const long end = p.prep == PG_PREP_GENOMES ? (long)p.n_genomes : (long)p.n_genomes + p.n_opponents;
+  if (net >= end) return;  // whole groups (HL divides 64)
   const WT *g;
   int flip;
   if (net < p.n_genomes) {
@@ -464,8 +472,16 @@ inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
   const int grid = want < cap ? want : cap;
   if (grid <= 0) return PG_OK;
   if (!p.recs) return fail(PG_ERR_INVALID, "split kernel: no lane-record workspace");
-  const long prep_threads = ((long)p.n_genomes + p.n_opponents) * (L / 2);
-  hipLaunchKernelGGL((k_prep_records<L, U, O, WT>), dim3((unsigned)((prep_threads + 255) / 256)), dim3(256), 0, s, p);
+  const long nets = p.prep == PG_PREP_GENOMES ? (long)p.n_genomes
+                   : (p.prep == PG_PREP_REST ? (long)p.n_opponents : (long)p.n_genomes + p.n_opponents);
+  const long prep_threads = nets * (L / 2);
+  // at least one block: it also zeroes the work header and the counters
+  const unsigned prep_blocks = (unsigned)((prep_threads + 255) / 256);
+  hipLaunchKernelGGL((k_prep_records<L, U, O, WT>), dim3(prep_blocks > 0 ? prep_blocks : 1u), dim3(256), 0, s, p);
+  if (p.prep == PG_PREP_GENOMES) {
+    PG_HIP(hipGetLastError());
+    return PG_OK;
+  }
   if (kSplitTrace && !p.trace)
     hipLaunchKernelGGL((k_service<L, U, O, WT, true>), dim3(grid), dim3(kSvcThreads), lds, s, p);
   else

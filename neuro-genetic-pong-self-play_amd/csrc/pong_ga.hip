@@ -968,6 +968,7 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     return fail(PG_ERR_INVALID, "precision=%d", a->precision);
   if (a->trace && (a->trace_games < 0 || a->trace_cap < 1))
     return fail(PG_ERR_INVALID, "trace needs trace_games >= 0 and trace_cap >= 1");
+  if (a->prep < PG_PREP_ALL || a->prep > PG_PREP_REST) return fail(PG_ERR_INVALID, "prep=%d", a->prep);
   const size_t need = pg_eval_workspace_bytes(a);
   if (!a->workspace || a->workspace_bytes < need)
     return fail(PG_ERR_INVALID, "workspace of %zu bytes required (got %zu)", need, a->workspace_bytes);
@@ -1006,8 +1007,14 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   p.bias = a->net.bias ? 1 : 0;
   p.max_width = max_width(a->net);
 
-  PG_HIP(hipMemsetAsync(a->workspace, 0, 256, s));
+  p.prep = a->prep;
   const int kernel = resolve_kernel(a);
+  if (kernel != PG_KERNEL_SPLIT) {
+    if (a->prep == PG_PREP_GENOMES) return PG_OK;  // no records outside the split kernel
+    p.prep = PG_PREP_ALL;
+    PG_HIP(hipMemsetAsync(a->workspace, 0, 256, s));
+    if (a->counters) PG_HIP(hipMemsetAsync(a->counters, 0, 16 * sizeof(uint64_t), s));
+  }  // the split kernel's k_prep_records zeroes the work header and the counters itself
   const bool res_ok = resident_shape_ok(a->net);
   const bool wide_ok = wide_shape_ok(a->net, a->n_games);
   if (kernel == PG_KERNEL_WIDE) {
@@ -1024,6 +1031,7 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     rc = a->net.dtype == PG_F64 ? launch_service_any<double>(p, L, a->net.nodes[2], s)
                                 : launch_service_any<float>(p, L, a->net.nodes[2], s);
     if (rc != PG_OK) return rc;
+    if (a->prep == PG_PREP_GENOMES) return PG_OK;  // records only: no games, no fitness
   } else if (kernel == PG_KERNEL_RESIDENT || kernel == PG_KERNEL_STAGED) {
 #ifndef PG_WITH_EXPERIMENTAL
     return fail(PG_ERR_UNSUPPORTED, "the %s kernel is an experimental layout, not in the product library "

@@ -16,12 +16,13 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 6
+PG_ABI_VERSION = 7
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
 PG_F32, PG_F64 = 0, 1
 PG_OPP_HARDCODED, PG_OPP_ROM_CPU, PG_OPP_SCORE, PG_OPP_NN = 0, 1, 2, 3
+PG_PREP_ALL, PG_PREP_GENOMES, PG_PREP_REST = 0, 1, 2
 PG_PREC_CERTIFIED, PG_PREC_F64 = 0, 1
 PG_SCHED_REFERENCE, PG_SCHED_SELFPLAY = 0, 1
 PG_KERNEL_AUTO, PG_KERNEL_GENERAL, PG_KERNEL_RESIDENT, PG_KERNEL_SPLIT, PG_KERNEL_WIDE, PG_KERNEL_STAGED = 0, 1, 2, 3, 4, 5
@@ -54,6 +55,7 @@ class PgEvalArgs(ctypes.Structure):
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
         ("hard_log", _vp), ("hard_cap", ctypes.c_int32), ("genome_rows", _vp),
         ("n_active", _vp),
+        ("prep", ctypes.c_int32),
     ]
 
 

@@ -15,6 +15,7 @@ import torch
 from . import _lib as L
 
 PRECISIONS = {"certified": L.PG_PREC_CERTIFIED, "f64": L.PG_PREC_F64}
+PREPS = {"all": L.PG_PREP_ALL, "genomes": L.PG_PREP_GENOMES, "rest": L.PG_PREP_REST}
 KERNELS = {"auto": L.PG_KERNEL_AUTO, "general": L.PG_KERNEL_GENERAL, "resident": L.PG_KERNEL_RESIDENT,
            "split": L.PG_KERNEL_SPLIT, "wide": L.PG_KERNEL_WIDE, "staged": L.PG_KERNEL_STAGED}
 DTYPES = {torch.float32: L.PG_F32, torch.float64: L.PG_F64}
@@ -106,7 +107,7 @@ class Evaluator:
                  out: Optional[EvalResult] = None, precision: Optional[str] = None,
                  kernel: Optional[str] = None, group_lanes: Optional[int] = None, validate: bool = True,
                  hard_log: Optional[torch.Tensor] = None, rows: Optional[torch.Tensor] = None,
-                 n_active: Optional[torch.Tensor] = None):
+                 n_active: Optional[torch.Tensor] = None, prep: str = "all"):
         """Run every genome's games to termination; returns (EvalResult, trace or None).
 
         ``validate`` checks the schedule's opponent rows on the host first (one
@@ -117,6 +118,11 @@ class Evaluator:
         indexed by i) -- eaSimple's ``invalid_ind`` without copying rows.
         ``n_active`` ([1] int32, device): play only entries i < n_active[0]
         (the others' results are left untouched).
+        ``prep`` (pg_eval_args.prep): "all"; "genomes" only prepares the split
+        kernel's genome records (no games: ``out`` is left untouched); "rest"
+        plays after such a call with the same genomes, rows, n_active and
+        evaluator (its workspace holds the records), preparing the opponents'
+        records first.
         """
         dev = self.device
         n = genomes.shape[0] if rows is None else rows.shape[0]
@@ -153,9 +159,8 @@ class Evaluator:
                 frames=torch.empty((n, games), dtype=torch.int32, device=dev),
                 total_frames=torch.empty((n, games), dtype=torch.float64, device=dev),
                 status=torch.empty(n, dtype=torch.int32, device=dev),
-                counters=torch.zeros(16, dtype=torch.int64, device=dev))
-        else:
-            out.counters.zero_()
+                counters=torch.empty(16, dtype=torch.int64, device=dev))
+        # (the counters are zeroed by pg_eval_population itself)
         trace = None
         if trace_games and trace_cap:
             trace = torch.zeros((trace_games, trace_cap), dtype=torch.uint8, device=dev)
@@ -186,6 +191,7 @@ class Evaluator:
             if hard_log.dim() != 2 or hard_log.shape[1] != 8:
                 raise ValueError("hard_log must be [cap, 8] int32")
             a.hard_log, a.hard_cap = _ptr(hard_log), hard_log.shape[0]
+        a.prep = PREPS[prep]
         a.kernel = KERNELS[kernel or self.kernel]
         a.group_lanes = self.group_lanes if group_lanes is None else int(group_lanes)
         ws = self._workspace(a)

@@ -86,6 +86,7 @@ class DeviceGA:
         self.profile = None      # dict: when set, step() adds per-phase wall ms (with device syncs)
         self._t_mark = self._t_sub = 0.0
         self._next = None        # (generation, inv, inherited): offspring already varied into spare[H:]
+        self.early_prep = True   # _early_prep: schedule + genome records during the hall-of-fame scan
         self.hard_log = None     # optional [cap, 8] int32: the evaluation's hard decisions (pg_eval_args.hard_log)
         self.on_evaluate = None  # optional callable(g, rows, opponents, result), right after each evaluation
         # Evaluation order: a genome's longest game sets when its last game ends,
@@ -413,7 +414,27 @@ class DeviceGA:
         inherited = self._buf("inherited", self.P, torch.float64)
         D.inherit(chosen, fitness, inherited, self.lineage_frames, self._lineage_alt)
         self.lineage_frames, self._lineage_alt = self._lineage_alt, self.lineage_frames
-        self._next = (g, inv, inherited, self._order(inv, g))
+        order = self._order(inv, g)
+        self._next = (g, inv, inherited, order, self._early_prep(g, store[self.H:], order))
+
+    def _early_prep(self, g: int, off: torch.Tensor, order):
+        """Generation g's schedule and its genomes' lane records, made before the
+        hall-of-fame scan (the device is idle during it) when neither needs the
+        updated hall of fame: a self-play schedule against a full hall of fame
+        (its size stays H, and self-play opponents are picked by index only).
+        Returns the schedule for _evaluate_fused, or None."""
+        n = self.hi - self.lo
+        if (not self.early_prep or self.schedule != "selfplay" or self.H == 0 or self.hof_n != self.H or self.last is None
+                or self.last.fitness.shape[0] != n):
+            return None
+        local, count = order
+        sched = D.schedule(self.schedule, n, self.n_games, self.lo, self.hof_fitness, self.H, self.seed, g,
+                           self.device, rows=local)
+        # the records land in the evaluator's workspace; the later PG_PREP_REST call
+        # (same genomes, rows, count; opponents of the same size) adds the opponents'
+        self.ev.evaluate(off, *sched, opponents=self.spare[: self.H], out=self.last, validate=False,
+                         hard_log=self.hard_log, rows=local, n_active=count, prep="genomes")
+        return sched
 
     def _order(self, inv_u8: Optional[torch.Tensor], g: int = 0):
         # by generation parity: generation g + 1's order is made while
@@ -424,18 +445,22 @@ class DeviceGA:
         D.order(n, self.lo, inv_u8, self.lineage_frames, self.order_by_length, local, count, self.ws)
         return local, count
 
-    def _evaluate_fused(self, g: int, rows: torch.Tensor, order) -> torch.Tensor:
+    def _evaluate_fused(self, g: int, rows: torch.Tensor, order, sched=None) -> torch.Tensor:
         lo, hi = self.lo, self.hi
         n = hi - lo
         local, count = order
-        kind, opp, mult = D.schedule(self.schedule, n, self.n_games, lo, self.hof_fitness, self.hof_n,
-                                     self.seed, g, self.device, rows=local)
+        if sched is None:
+            kind, opp, mult = D.schedule(self.schedule, n, self.n_games, lo, self.hof_fitness, self.hof_n,
+                                         self.seed, g, self.device, rows=local)
+        else:  # made during the hall-of-fame scan with the genomes' records (_early_prep)
+            kind, opp, mult = sched
         opponents = self.store[: self.hof_n] if self.hof_n else None
         out = self.last if (self.last is not None and self.last.fitness.shape[0] == n) else None
         if self.eval_events is not None:
             self.eval_events[0].record()
         res, _ = self.ev.evaluate(rows, kind, opp, mult, opponents=opponents, out=out, validate=False,
-                                  hard_log=self.hard_log, rows=local, n_active=count)
+                                  hard_log=self.hard_log, rows=local, n_active=count,
+                                  prep="all" if sched is None else "rest")
         if self.eval_events is not None:
             self.eval_events[1].record()
         self.last, self.last_rows, self.last_count = res, local, count
@@ -540,10 +565,10 @@ class DeviceGA:
         off = self.spare[self.H:]
         if self._next is None or self._next[0] != g:
             self._next_gen_prep(g, self.population, self.fitness, self.spare)
-        _, inv, inherited, order = self._next
+        _, inv, inherited, order, sched = self._next
         self._next = None
         self._mark("select_vary")
-        fit = self._evaluate_fused(g, off, order)  # invalid_ind only: clones keep their parent's fitness
+        fit = self._evaluate_fused(g, off, order, sched)  # invalid_ind only: clones keep their parent's fitness
         new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, inherited, worst)
         self._mark("evaluate")
         # generation g + 1's parents are this offspring; its offspring go to
