@@ -116,13 +116,13 @@ struct Pong {
     // left paddle: the action, or the built-in CPU of the 1-player env
     // (main.py:40) -- behind a wave-uniform test: no game of a self-play
     // schedule takes it
+    int nl = move_player(lpy, left_code);
     if (PG_ANY(one_player != 0)) {
       const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
       const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
-      lpy = one_player ? move(lpy, cpu_dy, kCpuSpeed) : move_player(lpy, left_code);
-    } else {
-      lpy = move_player(lpy, left_code);
+      nl = one_player ? move(lpy, cpu_dy, kCpuSpeed) : nl;
     }
+    lpy = nl;
 
     constexpr int ymax = kFieldH - kBallH;
     constexpr int lface = kLeftPaddleX + kPaddleW, rface = kRightPaddleX;
@@ -142,7 +142,11 @@ struct Pong {
     bx = fly ? nx : bx;
     by = fly ? ny : by;
     vy = fly ? wvy : vy;
-    if (PG_ANY(face) && face) {  // crossing a paddle face: bounce or miss
+    // the rare blocks -- a paddle face reached, the ball hidden -- behind one
+    // wave-uniform test (play is the state before this frame: the frame of a
+    // miss only starts the serve timer)
+    if (PG_ANY(face || !play)) {
+    if (face) {  // crossing a paddle face: bounce or miss
       const int py = to_left ? lpy : rpy;
       if ((ny <= py + kPaddleH - 1) && (ny + kBallH - 1 >= py)) {  // rows overlap: bounce
         hits += 1;
@@ -164,10 +168,11 @@ struct Pong {
         ev = kStepPoint;
       }
     }
-    if (PG_ANY(!play) && !play) {
+    if (!play) {
       // ball hidden: the serve timer runs down (the frame of a miss only starts it)
       timer = timer > 0 ? timer - 1 : 0;
       if (timer == 0 && !done()) serve_from(serve_of(point));
+    }
     }
     return ev;
   }

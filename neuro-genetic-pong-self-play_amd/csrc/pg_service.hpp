@@ -273,7 +273,10 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       if (idx < 0) idx = z[1] > z[0] ? 1 : 0;
 #endif
       PG_PP(pp_fail, idx < 0);
-      if (PG_ANY(idx < 0) && idx < 0) {  // rare, half-uniform: the memo, else ask the service wave
+      // rare, half-uniform: the in-wave plateau rule, then the memo, else ask
+      // the service wave (one wave-uniform test on the common path)
+      if (PG_ANY(idx < 0)) {
+      if (idx < 0) {
         fails += 1;
 #ifdef PG_TIMELINE
         g_fails += 1;
@@ -323,6 +326,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           }
         }
       }
+      }
       const int mine = index_to_code(idx);
       const int other = other_half<L>(mine);
       right = side ? other : mine;
@@ -343,12 +347,10 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
     }
 #endif
-    {  // calculate_timeout_and_frames (main.py:128-135); at most one point a frame
-      const bool same = ev != kStepPoint;  // a miss grows exactly one score
-      total += same ? 0 : timeout;
-      timeout = same ? timeout + 1 : 0;
-      if (PG_ANY(!same) && !same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
-    }
+    // calculate_timeout_and_frames (main.py:128-135); at most one point a frame
+    const bool same = ev != kStepPoint;  // a miss grows exactly one score
+    total += same ? 0 : timeout;
+    timeout = same ? timeout + 1 : 0;
 #ifndef PG_NO_RALLY_SKIP
     // a periodic rally ends at the timeout with nothing else changed: jump there
     // (never while tracing, which records every frame's actions)
@@ -369,9 +371,17 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // opening at the 8th return instead of at timeout 256, with a 64-frame
     // first span, fires at the cycle's first repetition in the common
     // two-bounce rally (tools/long_games.py: 460 instead of 610 frames).
-    const bool rally_check = bounced && st.hits >= kRallyHits && timeout <= kTimeoutThresh;
+    const bool rally_check = !kTracing && bounced && st.hits >= kRallyHits && timeout <= kTimeoutThresh;
+#else
+    constexpr bool rally_check = false;
+#endif
     PG_PP(pp_rally, rally_check);
-    if (!kTracing && PG_ANY(rally_check) && rally_check) {
+    bool over = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh;
+    // a point, a rally check or a game end: one wave-uniform test on the common path
+    if (PG_ANY(!same || rally_check || over)) {
+    if (!same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
+#ifndef PG_NO_RALLY_SKIP
+    if (rally_check) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
       const uint64_t key = rally_key(st, act_r, act_l);
       const int at = slots[rs].rally_at;
@@ -394,9 +404,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         }
       }
     }
+    over = over || timeout > kTimeoutThresh;  // a rally jump ends the game
 #endif
-    const bool over = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh;
-    if (PG_ANY(over) && over) {
+    if (over) {
       if (lig == 0) finish_game(p, w, st, frames, total);
 #ifdef PG_TIMELINE
       if (p.trace && w < p.trace_games && lig == 0) {
@@ -417,6 +427,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
       w = group_broadcast<L>(ww, leader);
       fresh = true;
+    }
     }
   }
   if (p.counters && c_games) {

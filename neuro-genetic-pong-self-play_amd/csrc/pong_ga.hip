@@ -1040,6 +1040,10 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     if (kernel == PG_KERNEL_STAGED) {
       if (!staged_shape_ok(a->net)) return fail(PG_ERR_UNSUPPORTED, "staged kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
       if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "staged kernel is the certified-precision path");
+      // k_prep_rows prepares the opponent records from the opponents table; a
+      // network game's opp row would otherwise index unprepared records
+      if (!a->opponents || a->n_opponents <= 0)
+        return fail(PG_ERR_UNSUPPORTED, "staged kernel needs an opponents table (use the split kernel)");
       rc = launch_staged(p, a, (char *)a->workspace + eval_base_workspace(a), s);
       if (rc != PG_OK) return rc;
     } else {
