@@ -111,13 +111,19 @@ struct Pong {
   // the same with the serves read from a table: serve_of(point) = serve_entry(seed, point)
   template <class ServeOf>
   __device__ int step(int right_code, int left_code, ServeOf serve_of) {
+    return step(right_code, left_code, serve_of, PG_ANY(one_player != 0));
+  }
+  // any_one_player: wave-uniform, true when some game of the wave may be a
+  // 1-player env (k_service keeps it from its game starts: no test per frame)
+  template <class ServeOf>
+  __device__ int step(int right_code, int left_code, ServeOf serve_of, bool any_one_player) {
     int ev = kStepFly;
     rpy = move_player(rpy, right_code);
     // left paddle: the action, or the built-in CPU of the 1-player env
     // (main.py:40) -- behind a wave-uniform test: no game of a self-play
     // schedule takes it
     int nl = move_player(lpy, left_code);
-    if (PG_ANY(one_player != 0)) {
+    if (__builtin_expect(any_one_player, 0)) {
       const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
       const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
       nl = one_player ? move(lpy, cpu_dy, kCpuSpeed) : nl;

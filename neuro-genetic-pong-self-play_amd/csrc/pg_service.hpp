@@ -166,6 +166,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     w = group_broadcast<L>(ww, leader);
   }
   bool fresh = true;
+  bool w_scripted = true, w_onep = true;  // wave-uniform; set at the first frame's starts
 #ifdef PG_START_PROBE  // diagnostic build: shader cycles of the game-start blocks vs the wave's total
   uint64_t probe_fresh = 0;
   const uint64_t probe_t0 = __builtin_amdgcn_s_memtime();
@@ -186,6 +187,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     const bool any_fresh = __builtin_amdgcn_ballot_w64(fresh) != 0;
     const uint64_t probe_f0 = __builtin_amdgcn_s_memtime();
 #endif
+    PG_PP(pp_frames, true);
+    // a game start or a hidden ball: one wave-uniform test on the common path
+    if (PG_ANY(fresh || !st.vis)) {
     if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
       const int i = w / p.n_games;
       const int g = w - i * p.n_games;
@@ -229,8 +233,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #endif
       const bool hid = !st.vis && st.timer >= 2;
       PG_PP(pp_hidden, hid);
-      PG_PP(pp_frames, true);
-      if (!kTrace && __builtin_amdgcn_ballot_w64(st.vis == 0) != 0 && hid) {
+      if (!kTrace && hid) {
         const int h = st.timer - 1;
         st.rpy = Pong::drift(st.rpy, h);
         if (!st.one_player) st.lpy = Pong::drift(st.lpy, h);
@@ -243,13 +246,18 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       }
     }
 #endif
+    // the wave's games after any start: is one of them scripted, or a
+    // 1-player env (both fixed for a game; no per-frame test otherwise)
+    w_scripted = PG_ANY(kind != kOppNN);
+    w_onep = PG_ANY(st.one_player != 0);
+    }
     const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
 #ifdef PG_PATH_PROBE
     const int pt_b = st.point, hits_b = st.hits;
 #endif
     const int ev = st.step(act_r, act_l, [&](int pt) {
       return tabbed && pt < kServeTabPoints ? serve_tab[tab_off + pt] : Pong::serve_entry(st.seed, pt);
-    });
+    }, w_onep);
     const bool bounced = ev == kStepBounce;  // a paddle returned the ball this frame
     PG_PP(pp_face, ev != kStepFly || st.hits != hits_b || st.point != pt_b);
     frames += 1;
@@ -333,7 +341,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       left = side ? mine : other;
       // HardcodedAi / ScoreHardcodedAi (dumb_ais.py): behind a wave-uniform
       // test, which a self-play schedule never passes
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!left_nn) != 0, 0) && !left_nn) {
+      if (__builtin_expect(w_scripted, 0) && !left_nn) {
         left = hardcoded(by2, lc2);
         if (kind == kOppScore && st.s1 > st.s2) left = 0;
       }
