@@ -4,6 +4,16 @@
 --config wide runs BASELINE config 5 instead: the same generation step for the
 wide MLP [6,512,512,3] (f32 genome storage, k_wide streaming kernel).
 
+Secondary runs:
+  --horizon T        the fixed-horizon measurement mode: every game slot runs
+                     exactly T frames with auto-reset, nothing advanced in
+                     closed form (pg_eval_args.horizon) -- the steady-state
+                     env-steps/s (main.py:76-107's frames, every one stepped);
+  --schedule reference  evaluate()'s own 6-game schedule (main.py:33-53: games
+                     0-2 scripted / the 1-player CPU, games 3-5 vs the hall of fame);
+  --dist init        U[0,1) genes (toolbox.attr_float = random.random, ga.py:85)
+                     instead of the "evolved" N(0, 3).
+
 One step = one GA generation of the reference's eaSimple loop
 (main.py:165-170) on device:
   1. evaluate every genome's 6 self-play games to termination
@@ -37,7 +47,7 @@ import torch.distributed as dist  # noqa: E402
 
 F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
-PROFILE_ROUND = "r03"           # profiles/<round>/ holds the PMC passes of the committed build
+PROFILE_ROUND = "r04"           # profiles/<round>/ holds the PMC passes of the committed build
 
 
 def parse():
@@ -54,9 +64,16 @@ def parse():
     p.add_argument("--group-lanes", type=int, default=0)
     p.add_argument("--kernel", default="auto")
     p.add_argument("--sigma", type=float, default=3.0)
+    p.add_argument("--dist", default="normal", choices=["normal", "init"],
+                   help="genes N(0, sigma) ('evolved', the headline) or U[0,1) ('init', ga.py:85)")
+    p.add_argument("--schedule", default="selfplay", choices=["selfplay", "reference"],
+                   help="selfplay: all-NN games vs the hall of fame (headline); reference: main.py:33-53's schedule")
+    p.add_argument("--horizon", type=int, default=0,
+                   help="T > 0: fixed-horizon mode, every game slot runs exactly T frames with auto-reset")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="CPU baseline pool: this box's CPU share per GPU (the pool's rule on a one-GPU box)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     a = p.parse_args()
     wide = a.config == "wide"
@@ -118,21 +135,25 @@ def main():
     # the device-resident eaSimple (pong_amd.evolve): replicated population,
     # rank r evaluates its shard, one all-gather of fitness per generation;
     # GA parameters are config.py's (cxpb = mutpb = indpb = alpha = sigma = 0.9, mu = 0)
-    ga = DeviceGA(shape, P, H, tournsize, dtype=dtype, device=dev, n_games=args.games, schedule="selfplay",
+    ga = DeviceGA(shape, P, H, tournsize, dtype=dtype, device=dev, n_games=args.games, schedule=args.schedule,
                   seed=args.seed, kernel=args.kernel)
     ga.ev.group_lanes = args.group_lanes
+    ga.ev.horizon = args.horizon  # pg_eval_args.horizon: 0 = evaluate()'s episodes
     ga.order_by_length = os.environ.get("PG_NO_LENGTH_ORDER") != "1"  # A/B switch for the evaluation order
     ga.early_prep = os.environ.get("PG_NO_EARLY_PREP") != "1"  # A/B switch: schedule + genome records during the HoF scan
     G = ga.G
-    ga.initialize("normal", args.sigma)
+    ga.initialize("normal" if args.dist == "normal" else "uniform", args.sigma)
     # the first games already face a full hall of fame: H independent random
     # genomes at fitness -1e300, which the first update replaces
     gen = torch.Generator(device=dev).manual_seed(args.seed + 1)
     rows = max(1, (1 << 28) // (8 * G))
     for r0 in range(0, H, rows):
         r1 = min(H, r0 + rows)
-        ga.store[r0:r1] = torch.randn((r1 - r0, G), generator=gen, dtype=torch.float64,
-                                      device=dev).mul_(args.sigma).to(dtype)
+        if args.dist == "normal":
+            blk = torch.randn((r1 - r0, G), generator=gen, dtype=torch.float64, device=dev).mul_(args.sigma)
+        else:
+            blk = torch.rand((r1 - r0, G), generator=gen, dtype=torch.float64, device=dev)
+        ga.store[r0:r1] = blk.to(dtype)
     ga.set_hall_of_fame(None, np.full(H, -1e300))
     lo = ga.lo
 
@@ -208,14 +229,16 @@ def main():
             cpu_pool.close()
         print(json.dumps(out), flush=True)
     elif rank == 0:
-        # env-steps = every frame of every game played to termination (what the
-        # reference steps env.step through, main.py:76-107): the frames stepped
-        # one at a time plus those advanced in closed form with the identical
-        # outcome (periodic rallies to their timeout, serve delays) -- results
-        # bit-identical to stepping each frame (tests/test_gpu_parity.py)
+        # value = env-steps STEPPED frame by frame (physics + obs + every NN
+        # forward of the frame) per second of wall time -- the
+        # definition of BENCH_r02.  The episode frames the reference's
+        # perform_episode loop runs (main.py:76-107) also count frames advanced
+        # in closed form with bit-identical outcomes (periodic rallies to their
+        # timeout, serve delays; tests/test_gpu_parity.py): a side field.
+        # --horizon T steps every frame of every game slot (no closed form).
         stepped_all = steps_all
-        steps_all = stepped_all + skip_all + hidden_all
-        env_steps_per_s = steps_all / elapsed
+        episode_all = stepped_all + skip_all + hidden_all
+        env_steps_per_s = stepped_all / elapsed
         ms_per_step = elapsed * 1000.0 / args.steps
         # roofline of the dominant kernel (k_service), per launch on rank 0's timing
         flops_per_forward = 2.0 * G
@@ -223,6 +246,10 @@ def main():
         steps_per_launch = stepped_all / world / args.steps
         achieved_tflops = fwd_per_launch * flops_per_forward / (kernel_ms_mean / 1e3) / 1e12
         streaming_bytes = steps_per_launch * (2 * 4 * G + 128)   # SURVEY 8d accounting, GB-equivalent
+        sched = ("self-play games vs the hall of fame" if args.schedule == "selfplay" else
+                 "evaluate()'s schedule (main.py:33-53: HardcodedAi, the 1-player CPU, ScoreHardcodedAi, 3 hall-of-fame games)")
+        mode = (f"fixed horizon: every game slot {args.horizon} frames, auto-reset (SURVEY 8d)" if args.horizon
+                else "every game to termination (evaluate())")
         out = {
             "metric": "env-steps/sec (GA evaluation loop, self-play) + generations/sec at pop=65536 per GPU",
             "value": env_steps_per_s,
@@ -236,18 +263,21 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 hidden + certified f64 argmax; genomes " + ("f64" if dtype == torch.float64 else "f32"),
-            "data": "synthetic N(0,%g) genomes, random-init [%s] MLPs, self-play vs hall of fame" % (args.sigma, args.shape),
-            "config": {"workload": "BASELINE config 3: population 65536 per GPU, MLP [6,64,3], 6 self-play games "
-                                   "per genome, device GA step (selTournament/varAnd/HoF)",
+            "data": "synthetic %s genomes, random-init [%s] MLPs, %s" % (
+                "N(0,%g)" % args.sigma if args.dist == "normal" else "U[0,1) (ga.py:85 init)", args.shape, sched),
+            "config": {"workload": "BASELINE config 3: population 65536 per GPU, MLP [6,64,3], 6 games per genome "
+                                   "(%s), device GA step (selTournament/varAnd/HoF); %s" % (sched, mode),
                        "population": P, "population_per_gpu": n_local, "network_shape": shape,
                        "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
+                       "schedule": args.schedule, "genes": args.dist, "horizon": args.horizon,
                        "parallelism": f"dp{world}" if world > 1 else "dp1",
-                   "process_group": (dist.get_backend() if dist.is_initialized() else None),
-                       "env_steps_definition": "episode frames: every frame of every game to termination; "
-                                               "value = their count / wall time",
-                       "env_steps_per_generation": steps_all / args.steps,
-                       "stepped_env_steps_per_generation": stepped_all / args.steps,
-                       "stepped_env_steps_per_sec": stepped_all / elapsed,
+                       "process_group": (dist.get_backend() if dist.is_initialized() else None),
+                       "env_steps_definition": "env-steps stepped one frame at a time (physics, observation and "
+                                               "every network forward of the frame); value = their count / wall "
+                                               "time (BENCH_r02's definition)",
+                       "env_steps_per_generation": stepped_all / args.steps,
+                       "episode_env_steps_per_sec": episode_all / elapsed,
+                       "episode_env_steps_per_generation": episode_all / args.steps,
                        "periodic_rally_frames_advanced_per_generation": skip_all / args.steps,
                        "serve_delay_frames_advanced_per_generation": hidden_all / args.steps,
                        "certificate_failures_per_forward": cert_all[0] / max(fwd_all, 1.0),
@@ -271,7 +301,7 @@ def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_pe
     """Roofline of k_service: compute-bound on the f32 vector ALU (VALU issue);
     HBM traffic from the committed PMC passes of the same build and command."""
     wt = 8 if dtype == torch.float64 else 4
-    pmc, src = _pmc("pmc_traffic.json")
+    pmc, src = _pmc(_pmc_name(args))
     traffic = pmc.get("traffic_bytes") if pmc else None
     stale = _pmc_stale(pmc)
     if stale:  # counters of another build: not this kernel's traffic
@@ -304,6 +334,13 @@ def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_pe
             "streaming_equivalent_frac_of_hbm": streaming_bytes / kernel_s / 1e9 / HBM_PEAK_GBS}
 
 
+def _pmc_name(args):
+    """The PMC summary of this run's workload: the headline's, or a secondary run's."""
+    tags = ([f"horizon{args.horizon}"] if args.horizon else []) + (["reference"] if args.schedule == "reference" else []) \
+        + (["init"] if args.dist == "init" else [])
+    return "pmc_traffic.json" if not tags else "pmc_traffic_%s.json" % "_".join(tags)
+
+
 def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed, steps_all, fwd_all, passes_all,
                 kernel_ms_mean, skip_all=0.0):
     """BASELINE config 5: the generation step with the wide MLP; k_wide is
@@ -323,7 +360,7 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
         traffic = None
     return {
         "metric": "env-steps/sec (GA evaluation loop, self-play, wide MLP) + generations/sec at pop=65536",
-        "value": (steps_all + skip_all) / elapsed,  # episode frames (periodic rallies advanced at once included)
+        "value": steps_all / elapsed,  # env-steps stepped frame by frame (periodic rallies jumped: a side field)
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -341,10 +378,11 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
                    "games_per_genome": args.games, "tournsize": tournsize, "hall_of_fame": H,
                    "parallelism": f"dp{world}" if world > 1 else "dp1",
                    "process_group": (dist.get_backend() if dist.is_initialized() else None),
-                   "env_steps_definition": "episode frames: every frame of every game to termination; "
-                                           "value = their count / wall time",
-                   "env_steps_per_generation": (steps_all + skip_all) / args.steps,
-                   "stepped_env_steps_per_generation": steps_all / args.steps,
+                   "env_steps_definition": "env-steps stepped one frame at a time (physics, observation and "
+                                           "every network forward of the frame); value = their count / wall time",
+                   "env_steps_per_generation": steps_all / args.steps,
+                   "episode_env_steps_per_sec": (steps_all + skip_all) / elapsed,
+                   "episode_env_steps_per_generation": (steps_all + skip_all) / args.steps,
                    "periodic_rally_frames_advanced_per_generation": skip_all / args.steps,
                    "network_passes_per_generation": passes_all / args.steps,
                    "forwards_per_network_pass": fwd_all / max(passes_all, 1.0)},

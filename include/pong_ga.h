@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 7
+#define PG_ABI_VERSION 8
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -99,16 +99,13 @@ typedef enum pg_precision {
 typedef enum pg_kernel {
   PG_KERNEL_AUTO = 0,      /* SPLIT when the shape and precision allow, else GENERAL */
   PG_KERNEL_GENERAL = 1,   /* one wave per game, f64, any NETWORK_SHAPE */
-  PG_KERNEL_RESIDENT = 2,  /* [6, H<=256, 2..4]: one lane group holds both paddles' weights */
+  PG_KERNEL_RESIDENT = 2,  /* retired (round 4): PG_ERR_UNSUPPORTED */
   PG_KERNEL_SPLIT = 3      /* [6, H<=256, 2..4]: half a lane group per paddle's network, plus one
                               f64 service wave per 1024-thread block for re-decisions */,
   PG_KERNEL_WIDE = 4,      /* [6, H1<=512, H2<=512, 1..4], n_games <= 8: one 512-thread workgroup per
                               genome plays its games in lockstep and streams W2 from HBM each frame
                               (numpy_nn's f64 order; AUTO picks it for H1 or H2 >= 64) */
-  PG_KERNEL_STAGED = 5     /* [6, H<=256, 2..4]: SPLIT's network lanes, with each block's physics and
-                              bookkeeping run by one environment wave (one lane per game) between the
-                              network stages; needs the larger workspace pg_eval_workspace_bytes()
-                              reports for it */
+  PG_KERNEL_STAGED = 5     /* retired (round 4): PG_ERR_UNSUPPORTED */
 } pg_kernel;
 
 /* pg_eval_args.prep: the SPLIT kernel's lane records (one per network of the
@@ -186,6 +183,16 @@ typedef struct pg_eval_args {
                                     and their counters, are left untouched) -- a count computed on the
                                     device needs no host round trip before the launch. */
   int32_t prep;                  /* pg_prep (ABI 7): PG_PREP_ALL unless the records are prepared in two calls */
+  int32_t horizon;               /* ABI 8, SURVEY 8(d)'s fixed-horizon measurement mode; 0 = off (evaluate()'s
+                                    episodes).  T > 0 (SPLIT kernel, [6, <=64, 3] networks only): every game slot
+                                    runs exactly T frames; an episode that terminates (main.py:102-107) before
+                                    frame T is scored (calculate_reward) and the slot auto-resets (a fresh
+                                    episode, the same networks, the serve sequence continuing), the partial
+                                    last episode is dropped; no frame is advanced in closed form (counters[0]
+                                    = n_games * T per genome, [8] = [12] = 0).  Outputs per game: rewards =
+                                    the sum of the completed episodes' rewards in order, scores = the points
+                                    of all its episodes (score1, score2), frames = T, total_frames = the
+                                    completed episodes, status = any ZeroDivisionError; fitness as usual. */
 } pg_eval_args;
 
 /* Trace byte: right_code | left_code << 2 | ball_visible << 4, where a code is
@@ -384,9 +391,8 @@ typedef struct pg_hof_prepare_args {
 
 const char *pg_version(void);
 int32_t pg_abi_version(void);
-/* Build options of this library: bit 0 = the experimental evaluation layouts
- * (PG_KERNEL_RESIDENT, PG_KERNEL_STAGED) are compiled in; without them those
- * kernels return PG_ERR_UNSUPPORTED. */
+/* Build options of this library (0: no optional features; the retired layouts
+ * PG_KERNEL_RESIDENT / PG_KERNEL_STAGED are never compiled in). */
 int32_t pg_build_flags(void);
 const char *pg_last_error(void);
 /* Number of visible HIP devices (>= 0), or a negative pg_status. */

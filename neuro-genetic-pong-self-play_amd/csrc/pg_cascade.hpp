@@ -1,6 +1,6 @@
 // pg_cascade.hpp -- the certified f32 forward of the game networks and its
-// decision cascade, shared by the evaluation kernels (k_resident, k_service in
-// pong_ga.hip; k_staged in pg_staged.hip) and pg_decide:
+// decision cascade, shared by k_service (pg_service.hpp), the batched forward
+// k_forward_resident (pg_forward) and pg_decide:
 //   load_net / load_net_pk   a lane's share of a [6, H, O] network in VGPRs
 //                            (numpy_nn.py:52-69 gene layout) + the f32 bound
 //   partial_f32 / partial_pk the hidden layer and lane-partial output sums
@@ -20,7 +20,7 @@
 
 namespace pg {
 
-// ================================================== resident (fast) path ==
+// ======================================= one network per lane group (pg_forward) ==
 #ifndef PG_SLOW_INLINE
 #define PG_SLOW_INLINE __forceinline__
 #endif
@@ -512,57 +512,6 @@ __device__ PG_SLOW_INLINE int forward_f64_group(const WT *__restrict__ g, int H,
 
 __device__ __forceinline__ float feat32(int k) { return (float)k * 0.003125f; }  // k / 320, <= 2u rel. error
 
-// One frame's decisions: the right paddle's network always, the left paddle's
-// when it is a network too (self-play / hall-of-fame games).  The two f32
-// passes are independent, so their hidden layers and reductions interleave.
-// Any undecided argmax is re-decided by ONE f64 code site (keeps the rare
-// path's registers and code out of the hot loop's way).
-template <int L, int U, int O, typename WT>
-__device__ __forceinline__ int2 decide(Net<U, O> &nr, const WT *gr, const int kr[6], Net<U, O> &nl,
-                                       const WT *gl, const int kl[6], bool left_nn, int left_scripted, int H,
-                                       int b, double *lds, int lig, uint32_t &slow) {
-  float xr[6], ar[O], zr[O], zl[O];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) xr[i] = feat32(kr[i]);
-  partial_f32<U, O>(nr, xr, ar);
-  int il = 0;
-  if (left_nn) {
-    float xl[6], al[O];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) xl[i] = feat32(kl[i]);
-    partial_f32<U, O>(nl, xl, al);
-#pragma unroll
-    for (int o = 0; o < O; ++o) {
-      zr[o] = group_sum<L>(ar[o]) + nr.c[o];
-      zl[o] = group_sum<L>(al[o]) + nl.c[o];
-    }
-    il = certify<O>(zl, nl.e);
-  } else {
-#pragma unroll
-    for (int o = 0; o < O; ++o) zr[o] = group_sum<L>(ar[o]) + nr.c[o];
-  }
-  int ir = certify<O>(zr, nr.e);
-#ifdef PG_ABLATE_CERT  // timing-only build: plain f32 argmax, no certification
-  ir = zr[1] > zr[0] ? 1 : 0;
-  if (left_nn) il = zl[1] > zl[0] ? 1 : 0;
-#endif
-  if (ir < 0 || il < 0) {  // rare and group-uniform
-    if (il < 0) {
-      il = forward_f64_group<L, U, O, WT>(gl, H, b, kl, lds, lig);
-      slow += 1;
-    }
-    if (ir < 0) {
-      ir = forward_f64_group<L, U, O, WT>(gr, H, b, kr, lds, lig);
-      slow += 1;
-    }
-    // Re-read the weights instead of keeping them live across the f64 pass:
-    // the rare path then does not add its registers to the hot loop's budget.
-    load_net<L, U, O, WT>(nr, gr, H, b, lig);
-    if (left_nn) load_net<L, U, O, WT>(nl, gl, H, b, lig);
-  }
-  return make_int2(index_to_code(ir), left_nn ? index_to_code(il) : left_scripted);
-}
-
 template <int L>
 __device__ __forceinline__ int group_broadcast(int v, int leader_lane) {
   if constexpr (L == 64) return __builtin_amdgcn_readfirstlane(v);
@@ -635,6 +584,10 @@ struct SlowSlot {
   int memo_idx[kMemo];
   uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
   int rally_at, rally_span;
+  // fixed-horizon mode (pg_eval_args.horizon; side-0 slot): the completed
+  // episodes' reward sum, count and ZeroDivisionError flag, every episode's points
+  double hz_sum;
+  int hz_eps, hz_s1, hz_s2, hz_zd;
 };
 
 // The plateau certificate in f32, tried by the game wave itself where

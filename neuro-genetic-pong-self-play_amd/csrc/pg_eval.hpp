@@ -47,6 +47,7 @@ struct EvalParams {
   int nodes[PG_MAX_NODES];
   int n_nodes, bias, max_width;
   float *recs;         // split kernel: lane records (k_prep_records), [n_genomes + n_opponents][L/2][rec_floats]
+  int horizon;         // pg_eval_args.horizon: fixed-horizon measurement mode (T frames per game slot), 0 = off
   int prep;            // pg_prep: which records k_prep_records writes; it also zeroes the work header and
                        // the counters when its launch precedes the games (PG_PREP_ALL / PG_PREP_REST)
   void *wide_scratch;  // k_wide: the blocks' tile-major W2 copies (workspace)
@@ -76,22 +77,23 @@ __device__ inline int genome_row(const EvalParams &p, int i) { return p.rows ? p
 
 // Results of one finished game: perform_episode's return value and the
 // bookkeeping around it (main.py:108-112, utils.py:104-109).
-__device__ inline void finish_game(const EvalParams &p, int w, const Pong &st, int frames, int total) {
-  const double mult = p.mult[w];
-  double reward = 0.0;
-  int zero_div = 0;
-  if (st.s1 != st.s2) {
-    const double tf = (double)total;
-    if (tf == 0.0) {
-      zero_div = 1;
-      reward = __builtin_nan("");
-    } else {
-      // ((my - enemy) + my * mult) / (total_frames / 100.0), no contraction
-      const double diff = (double)(st.s2 - st.s1);
-      const double bonus = __dmul_rn((double)st.s2, mult);
-      reward = __dadd_rn(diff, bonus) / (tf / 100.0);
-    }
+__device__ inline double episode_reward(const Pong &st, int total, double mult, int &zero_div) {
+  zero_div = 0;
+  if (st.s1 == st.s2) return 0.0;  // main.py:109-110
+  const double tf = (double)total;
+  if (tf == 0.0) {
+    zero_div = 1;
+    return __builtin_nan("");
   }
+  // ((my - enemy) + my * mult) / (total_frames / 100.0), no contraction
+  const double diff = (double)(st.s2 - st.s1);
+  const double bonus = __dmul_rn((double)st.s2, mult);
+  return __dadd_rn(diff, bonus) / (tf / 100.0);
+}
+
+__device__ inline void finish_game(const EvalParams &p, int w, const Pong &st, int frames, int total) {
+  int zero_div;
+  const double reward = episode_reward(st, total, p.mult[w], zero_div);
   p.rewards[w] = reward;
   p.scores[2 * w] = st.s1;
   p.scores[2 * w + 1] = st.s2;
@@ -129,10 +131,5 @@ bool wide_shape_ok(const pg_net &n, int n_games);
 size_t wide_workspace_bytes(const pg_eval_args *a);
 int32_t launch_wide(const EvalParams &p, int dtype, void *scratch, hipStream_t s);
 
-// [6, H<=256, 2..4] networks on the two-stage kernel k_staged (pg_staged.hip):
-// its extra workspace (prepared lane records of every row) and the launch.
-bool staged_shape_ok(const pg_net &n);
-size_t staged_workspace_bytes(const pg_eval_args *a);
-int32_t launch_staged(const EvalParams &p, const pg_eval_args *a, void *prep, hipStream_t s);
 
 }  // namespace pg

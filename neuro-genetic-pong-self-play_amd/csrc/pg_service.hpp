@@ -55,8 +55,11 @@ __global__ __launch_bounds__(256) void k_prep_records(EvalParams p) {
 }
 
 // kUntraced: a launch without a trace buffer (the GA's), the trace tests
-// compiled out of the frame instead of tested on p.trace every frame
-template <int L, int U, int O, typename WT, bool kUntraced = false>
+// compiled out of the frame instead of tested on p.trace every frame.
+// kHorizon: SURVEY 8(d)'s fixed-horizon measurement mode (pg_eval_args.horizon,
+// untraced): every game slot runs exactly p.horizon frames, episodes auto-reset,
+// nothing is advanced in closed form.
+template <int L, int U, int O, typename WT, bool kUntraced = false, bool kHorizon = false>
 __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   constexpr int kSvcThreads = svc_threads<U>();
   constexpr int kSvcGameWaves = kSvcThreads / 64 - 1;
@@ -210,6 +213,10 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       fresh = false;
       if (hl == 0) slots[sx].n_memo = 0;
       if (lig == 0) slots[sx].rally_at = -1;  // (sx is the side-0 slot there)
+      if (kHorizon && lig == 0) {
+        slots[sx].hz_sum = 0.0;
+        slots[sx].hz_eps = slots[sx].hz_s1 = slots[sx].hz_s2 = slots[sx].hz_zd = 0;
+      }
 #ifdef PG_TIMELINE  // experiment build: per-game wall-clock start/end into p.trace
       t_start = wall_clock64();
       g_fails = g_slow = 0;
@@ -233,7 +240,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #endif
       const bool hid = !st.vis && st.timer >= 2;
       PG_PP(pp_hidden, hid);
-      if (!kTrace && hid) {
+      if (!kTrace && !kHorizon && hid) {
         const int h = st.timer - 1;
         st.rpy = Pong::drift(st.rpy, h);
         if (!st.one_player) st.lpy = Pong::drift(st.lpy, h);
@@ -379,12 +386,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // opening at the 8th return instead of at timeout 256, with a 64-frame
     // first span, fires at the cycle's first repetition in the common
     // two-bounce rally (tools/long_games.py: 460 instead of 610 frames).
-    const bool rally_check = !kTracing && bounced && st.hits >= kRallyHits && timeout <= kTimeoutThresh;
+    const bool rally_check = !kTracing && !kHorizon && bounced && st.hits >= kRallyHits && timeout <= kTimeoutThresh;
 #else
     constexpr bool rally_check = false;
 #endif
     PG_PP(pp_rally, rally_check);
     bool over = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh;
+    if constexpr (kHorizon) over = over || frames >= p.horizon;
     // a point, a rally check or a game end: one wave-uniform test on the common path
     if (PG_ANY(!same || rally_check || over)) {
     if (!same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
@@ -414,8 +422,44 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     }
     over = over || timeout > kTimeoutThresh;  // a rally jump ends the game
 #endif
+    if constexpr (kHorizon) {
+      if (over) {  // an episode's end or the horizon's
+        const int rs = (threadIdx.x / L) * 2;
+        const bool ep_end = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh;
+        if (lig == 0) {
+          if (ep_end) {  // perform_episode's reward (main.py:108-112), summed in episode order
+            int zd;
+            slots[rs].hz_sum = __dadd_rn(slots[rs].hz_sum, episode_reward(st, total, p.mult[w], zd));
+            slots[rs].hz_zd |= zd;
+            slots[rs].hz_eps += 1;
+          }
+          slots[rs].hz_s1 += st.s1;
+          slots[rs].hz_s2 += st.s2;
+        }
+        if (ep_end && frames < p.horizon) {  // auto-reset: a fresh episode in the slot, the serves continuing
+          const int pt = st.point;
+          st.reset(st.seed, st.one_player);
+          st.point = pt;
+          act_r = act_l = total = 0;
+          timeout = -1;
+          over = false;
+        }
+      }
+    }
     if (over) {
-      if (lig == 0) finish_game(p, w, st, frames, total);
+      if constexpr (kHorizon) {
+        if (lig == 0) {
+          const int rs = (threadIdx.x / L) * 2;
+          p.rewards[w] = slots[rs].hz_sum;
+          p.scores[2 * w] = slots[rs].hz_s1;
+          p.scores[2 * w + 1] = slots[rs].hz_s2;
+          p.frames[w] = frames;
+          p.total_frames[w] = (double)slots[rs].hz_eps;
+          p.status_game[w] = slots[rs].hz_zd;
+        }
+      } else {
+        if (lig == 0) finish_game(p, w, st, frames, total);
+      }
 #ifdef PG_TIMELINE
       if (p.trace && w < p.trace_games && lig == 0) {
         uint32_t *tl = (uint32_t *)(p.trace + (long)w * p.trace_cap);
@@ -491,6 +535,8 @@ inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
   const int grid = want < cap ? want : cap;
   if (grid <= 0) return PG_OK;
   if (!p.recs) return fail(PG_ERR_INVALID, "split kernel: no lane-record workspace");
+  if (!kSplitTrace && p.horizon > 0)
+    return fail(PG_ERR_UNSUPPORTED, "horizon mode: [6, 33..64, 3] networks on 8-lane groups only");
   const long nets = p.prep == PG_PREP_GENOMES ? (long)p.n_genomes
                    : (p.prep == PG_PREP_REST ? (long)p.n_opponents : (long)p.n_genomes + p.n_opponents);
   const long prep_threads = nets * (L / 2);
@@ -501,7 +547,9 @@ inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
     PG_HIP(hipGetLastError());
     return PG_OK;
   }
-  if (kSplitTrace && !p.trace)
+  if (kSplitTrace && p.horizon > 0)  // the fixed-horizon mode: the bench layout's untraced instance
+    hipLaunchKernelGGL((k_service<L, U, O, WT, true, true>), dim3(grid), dim3(kSvcThreads), lds, s, p);
+  else if (kSplitTrace && !p.trace)
     hipLaunchKernelGGL((k_service<L, U, O, WT, true>), dim3(grid), dim3(kSvcThreads), lds, s, p);
   else
     hipLaunchKernelGGL((k_service<L, U, O, WT, false>), dim3(grid), dim3(kSvcThreads), lds, s, p);

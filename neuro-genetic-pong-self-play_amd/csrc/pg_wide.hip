@@ -67,9 +67,23 @@ constexpr int kStreamPolicy = 2;
 #endif
 
 // LDS carve (bytes): feats [NC][8] f64 | outputs [NC][4] f64 | control |
-// opponent rows | rally keys | h1 [C2][NC] f64 (W3 staging after layer 2) |
-// h2 [C3][NC] f64 | when they fit: every network's W3 [NG + 1][O][C3] WT.
-constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffRally = 2048, kOffH1 = 2304;
+// opponent rows | rally keys | game states [NG] WideGame | h1 [C2][NC] f64
+// (W3 staging after layer 2) | h2 [C3][NC] f64 | when they fit: every
+// network's W3 [NG + 1][O][C3] WT.
+constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffRally = 2048, kOffGames = 2304,
+              kOffH1 = 3328;
+
+// One game's state between frames, kept in LDS by wave 0 (lane c = game c)
+// instead of in VGPRs: every wave of the block carries the frame loop's
+// registers, and ~30 of them live across layers 1-3 only for wave 0's
+// phases A and E had been spilled around the W2 stream.
+struct WideGame {
+  Pong st;
+  int act_r, act_l, timeout, total, frames, kind, w, active;
+  int s1b, s2b, vis, lc2, rc2, left, pad0, pad1;  // this frame's, from phase A to phase E
+};
+static_assert(sizeof(WideGame) == 128, "WideGame: 8 x 16 B");
+static_assert(kOffGames + kWideMaxGames * (int)sizeof(WideGame) <= kOffH1, "LDS carve");
 __host__ __device__ constexpr int align16(int v) { return (v + 15) & ~15; }
 
 __host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b) {
@@ -237,6 +251,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   int *ctl = (int *)(lds_raw + kOffCtl);         // [0] genome; frame-parity halves at [8..] and [40..]
   long long *orow = (long long *)(lds_raw + kOffOrow);  // [NG] opponent row offsets (elements)
   uint64_t *rkey = (uint64_t *)(lds_raw + kOffRally);    // [NG] Brent's saved rally key per game
+  WideGame *games = (WideGame *)(lds_raw + kOffGames);    // [NG] the games' states (wave 0)
   int *rat = (int *)(lds_raw + kOffRally + 64), *rspan = (int *)(lds_raw + kOffRally + 96);
   double *h1 = (double *)(lds_raw + kOffH1);            // [C2][NC]
   double *h2 = (double *)(lds_raw + kOffH1 + align16(C2 * NC * 8));  // [C3][NC]
@@ -262,22 +277,24 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
     const int grow = genome_row(p, gi);
     const WT *gbase = genomes + (long)grow * p.gstride;
 
-    // game state: wave 0, lane g < n_games
-    Pong st;
-    int act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0, kind = 0, w = 0;
-    bool active = false;
+    // game state: wave 0, lane g < n_games, in LDS between the phases (WideGame)
     if (wid == 0 && lane < n_games) {
-      w = gi * n_games + lane;
+      WideGame g;
+      g.w = gi * n_games + lane;
       // probe (pg_wide_decide): one scripted-opponent "game" whose single frame
       // is the genome on the given features
-      kind = probe ? kOppHard : p.kind[w];
-      orow[lane] = kind == kOppNN ? (long long)p.opp[w] * p.ostride : 0;
-      st.reset(game_seed(p.seed, lane), kind == kOppRomCpu);
+      g.kind = probe ? kOppHard : p.kind[g.w];
+      orow[lane] = g.kind == kOppNN ? (long long)p.opp[g.w] * p.ostride : 0;
+      g.st.reset(game_seed(p.seed, lane), g.kind == kOppRomCpu);
+      g.act_r = g.act_l = g.timeout = g.total = g.frames = 0;
+      g.active = 1;
+      g.s1b = g.s2b = g.vis = g.lc2 = g.rc2 = g.left = g.pad0 = g.pad1 = 0;
+      games[lane] = g;
       rat[lane] = -1;  // no rally search open
-      active = true;
     }
     if (wid == 0) {
-      const uint64_t nb = __ballot(lane < n_games && kind == kOppNN);
+      const bool nng = lane < n_games && !probe && p.kind[gi * n_games + (lane < n_games ? lane : 0)] == kOppNN;
+      const uint64_t nb = __ballot(nng);
       if (lane == 0) ctl[1] = 1 | (int)((unsigned)nb << 1);  // networks to re-lay: bit 0 genome, 1 + c opponents
     }
     __syncthreads();
@@ -286,43 +303,49 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
     for (int fno = 0;; ++fno) {  // frames, all games in lockstep
       int *cf = ctl + 8 + (fno & 1) * 32;  // [0] column mask, [1] any active, [2] nets, [3..] net ids
       // ---- A: env.step + find_stuff + inference features (main.py:77-87)
-      int s1b = 0, s2b = 0, vis = 0, lc2 = 0, rc2 = 0, left = 0;
       if (wid == 0) {
+        const bool mine = lane < n_games;
+        WideGame g;
+        if (mine) g = games[lane];
+        const bool active = mine && g.active;
         if (active && probe) {  // the given doubled centroids (log_wide's k) in place of a frame
-          vis = 1;
+          g.vis = 1;
           const int32_t *kk = p.wide_probe_k + (long)gi * 6;
           double *fr = feat + lane * 8;
 #pragma unroll
           for (int i = 0; i < 6; ++i) fr[i] = feat64(kk[i]);
           fr[6] = 1.0;
         } else if (active) {
-          s1b = st.s1;
-          s2b = st.s2;
+          Pong &st = g.st;
+          g.s1b = st.s1;
+          g.s2b = st.s2;
           const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
-          st.step(act_r, act_l);
-          frames += 1;
-          vis = st.vis;
+          st.step(g.act_r, g.act_l);
+          g.frames += 1;
+          g.vis = st.vis;
           const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
-          lc2 = paddle_c2(st.lpy);
-          rc2 = paddle_c2(st.rpy);
-          if (vis) {  // get_actions main.py:143-150
+          g.lc2 = paddle_c2(st.lpy);
+          g.rc2 = paddle_c2(st.rpy);
+          g.left = 0;
+          if (g.vis) {  // get_actions main.py:143-150
             const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
             double *fr = feat + lane * 8;
             fr[0] = feat64(bx2); fr[1] = feat64(by2); fr[2] = feat64(lbx2);
-            fr[3] = feat64(lby2); fr[4] = feat64(rc2); fr[5] = feat64(lc2); fr[6] = 1.0;
-            if (kind == kOppNN) {
+            fr[3] = feat64(lby2); fr[4] = feat64(g.rc2); fr[5] = feat64(g.lc2); fr[6] = 1.0;
+            if (g.kind == kOppNN) {
               double *fl = feat + (NG + lane) * 8;
               fl[0] = feat64_flip(bx2); fl[1] = feat64(by2); fl[2] = feat64_flip(lbx2);
-              fl[3] = feat64(lby2); fl[4] = feat64(lc2); fl[5] = feat64(rc2); fl[6] = 1.0;
-            } else if (kind == kOppScore) {
-              left = (st.s1 <= st.s2) ? hardcoded(by2, lc2) : 0;
+              fl[3] = feat64(lby2); fl[4] = feat64(g.lc2); fl[5] = feat64(g.rc2); fl[6] = 1.0;
+            } else if (g.kind == kOppScore) {
+              g.left = (st.s1 <= st.s2) ? hardcoded(by2, g.lc2) : 0;
             } else {
-              left = hardcoded(by2, lc2);
+              g.left = hardcoded(by2, g.lc2);
             }
           }
         }
-        const uint64_t rb = __ballot(active && vis);
-        const uint64_t lb = __ballot(active && vis && kind == kOppNN);
+        if (active) games[lane] = g;
+        const uint64_t rb = __ballot(active && g.vis);
+        const uint64_t lb = __ballot(active && g.vis && g.kind == kOppNN);
         const uint64_t ab = __ballot(active);
         if (lane == 0) {
           cf[0] = (int)((unsigned)rb | ((unsigned)lb << NG));
@@ -688,65 +711,71 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       }
 
       // ---- E: actions, clamp, bookkeeping (main.py:88-107, 128-135)
-      if (wid == 0 && active && probe) {
-        p.wide_probe_index[gi] = argmax_np(outv, O);
-        if (p.wide_probe_act)
-          for (int o = 0; o < O; ++o) p.wide_probe_act[(long)gi * O + o] = outv[o];
-        active = false;
-      } else if (wid == 0 && active) {
-        int right = 0;
-        if (vis) {
-          const int ir = argmax_np(outv + lane * 4, O);
-          right = index_to_code(ir);
-          if (p.hard_log && near_tie(outv + lane * 4, O)) log_wide(p.hard_log, p.counters, p.hard_cap, grow, 0, ir, feat + lane * 8);
-          if (kind == kOppNN) {
-            const int il = argmax_np(outv + (NG + lane) * 4, O);
-            left = index_to_code(il);
-            if (p.hard_log && near_tie(outv + (NG + lane) * 4, O)) log_wide(p.hard_log, p.counters, p.hard_cap, p.opp[w], 1, il, feat + (NG + lane) * 8);
+      if (wid == 0 && lane < n_games) {
+        WideGame g = games[lane];
+        if (g.active && probe) {
+          p.wide_probe_index[gi] = argmax_np(outv, O);
+          if (p.wide_probe_act)
+            for (int o = 0; o < O; ++o) p.wide_probe_act[(long)gi * O + o] = outv[o];
+          g.active = 0;
+        } else if (g.active) {
+          Pong &st = g.st;
+          const int w = g.w;
+          int right = 0, left = g.left;
+          if (g.vis) {
+            const int ir = argmax_np(outv + lane * 4, O);
+            right = index_to_code(ir);
+            if (p.hard_log && near_tie(outv + lane * 4, O)) log_wide(p.hard_log, p.counters, p.hard_cap, grow, 0, ir, feat + lane * 8);
+            if (g.kind == kOppNN) {
+              const int il = argmax_np(outv + (NG + lane) * 4, O);
+              left = index_to_code(il);
+              if (p.hard_log && near_tie(outv + (NG + lane) * 4, O)) log_wide(p.hard_log, p.counters, p.hard_cap, p.opp[w], 1, il, feat + (NG + lane) * 8);
+            }
+            c_fwd += 1 + (g.kind == kOppNN ? 1 : 0);
           }
-          c_fwd += 1 + (kind == kOppNN ? 1 : 0);
-        }
-        act_l = clamp_action(lc2, left);
-        act_r = clamp_action(rc2, right);
-        if (p.trace && w < p.trace_games && frames <= p.trace_cap)
-          p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
-        if (frames > 1) {
-          if (st.s1 == s1b && st.s2 == s2b) {
-            timeout += 1;
-          } else {
-            total += timeout;
-            timeout = 0;
-            rat[lane] = -1;  // a point: the next rally searches afresh
+          g.act_l = clamp_action(g.lc2, left);
+          g.act_r = clamp_action(g.rc2, right);
+          if (p.trace && w < p.trace_games && g.frames <= p.trace_cap)
+            p.trace[(long)w * p.trace_cap + g.frames - 1] = (uint8_t)(g.act_r | (g.act_l << 2) | (g.vis << 4));
+          if (g.frames > 1) {
+            if (st.s1 == g.s1b && st.s2 == g.s2b) {
+              g.timeout += 1;
+            } else {
+              g.total += g.timeout;
+              g.timeout = 0;
+              rat[lane] = -1;  // a point: the next rally searches afresh
+            }
           }
-        }
 #ifndef PG_NO_RALLY_SKIP
-        // a periodic rally ends at the timeout with nothing else changed (pg_device.hpp
-        // rally_key); no state of a point recurs before its kRallyHits-th return
-        if (st.hits >= kRallyHits && timeout <= kTimeoutThresh && (timeout & (kRallyStride - 1)) == 0 &&
-            !p.trace) {
-          const uint64_t key = rally_key(st, act_r, act_l);
-          if (rat[lane] < 0) {
-            rkey[lane] = key;
-            rat[lane] = timeout;
-            rspan[lane] = kRallySpan0;
-          } else if (rkey[lane] == key) {
-            const int rest = kTimeoutThresh + 1 - timeout;
-            frames += rest;
-            c_skip += rest;
-            timeout = kTimeoutThresh + 1;
-          } else if (timeout - rat[lane] >= rspan[lane]) {
-            rkey[lane] = key;
-            rat[lane] = timeout;
-            rspan[lane] *= 2;
+          // a periodic rally ends at the timeout with nothing else changed (pg_device.hpp
+          // rally_key); no state of a point recurs before its kRallyHits-th return
+          if (st.hits >= kRallyHits && g.timeout <= kTimeoutThresh && (g.timeout & (kRallyStride - 1)) == 0 &&
+              !p.trace) {
+            const uint64_t key = rally_key(st, g.act_r, g.act_l);
+            if (rat[lane] < 0) {
+              rkey[lane] = key;
+              rat[lane] = g.timeout;
+              rspan[lane] = kRallySpan0;
+            } else if (rkey[lane] == key) {
+              const int rest = kTimeoutThresh + 1 - g.timeout;
+              g.frames += rest;
+              c_skip += rest;
+              g.timeout = kTimeoutThresh + 1;
+            } else if (g.timeout - rat[lane] >= rspan[lane]) {
+              rkey[lane] = key;
+              rat[lane] = g.timeout;
+              rspan[lane] *= 2;
+            }
+          }
+#endif
+          if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || g.timeout > kTimeoutThresh) {
+            finish_game(p, w, st, g.frames, g.total);
+            g.active = 0;
+            c_steps += g.frames;
+            c_games += 1;
           }
         }
-#endif
-        if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
-          finish_game(p, w, st, frames, total);
-          active = false;
-          c_steps += frames;
-          c_games += 1;
-        }
+        games[lane] = g;
       }
     }
   }

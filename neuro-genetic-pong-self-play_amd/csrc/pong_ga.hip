@@ -6,11 +6,10 @@
 // registers for the whole episode, so HBM is touched once per game (weights
 // in, results out) instead of once per frame.  See DESIGN.md.
 //
-//   k_resident<L,U,O,WT>  [6, H<=L*U, O] networks: an aligned group of L lanes
-//                         plays one game; lane l holds hidden units l, l+L, ..
-//                         (U per lane) of both paddles' networks in VGPRs; the
-//                         output dot products are DPP/shuffle group reductions.
-//                         f32 math with a certified f64 argmax (see certify()).
+//   k_service<L,U,O,WT>   [6, H<=256, O] networks (pg_service.hpp): an aligned
+//                         group of L lanes plays one game, half a group per
+//                         paddle's network in VGPRs, one f64 service wave per
+//                         block; f32 math with a certified f64 argmax.
 //   k_general<WT>         any NETWORK_SHAPE, one wave per game, f64 numpy_nn
 //                         arithmetic with activations staged in LDS.
 //   k_fitness             sum(all_rewards) / GAMES_TO_PLAY in the reference order.
@@ -180,108 +179,6 @@ __global__ __launch_bounds__(64) void k_general(EvalParams p) {
   }
 }
 
-// (the resident path's and the split path's device helpers live in pg_cascade.hpp)
-
-#ifdef PG_WITH_EXPERIMENTAL  // k_resident: an alternative layout kept out of the product build
-template <int L, int U, int O, typename WT>
-__global__ PG_RES_BOUNDS void k_resident(EvalParams p) {
-  const int H = p.nodes[1];
-  const int b = p.bias;
-  extern __shared__ double lds_all[];
-  const int lane64 = threadIdx.x & 63;
-  const int lig = threadIdx.x & (L - 1);
-  const int grp = threadIdx.x / L;
-  const int leader = lane64 & ~(L - 1);
-  double *lds = lds_all + grp * f64_lds_doubles(H, O);
-  const WT *genomes = (const WT *)p.genomes;
-  const WT *opponents = (const WT *)p.opponents;
-
-  Net<U, O> nr, nl;
-  Pong st;
-  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0;
-  const WT *gr = genomes, *gl = genomes;
-  uint32_t slow = 0, c_fwd = 0;
-  uint64_t c_steps = 0, c_games = 0;
-
-  const int games_total = active_total(p);
-  int w;
-  {
-    int ww = 0;
-    if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
-    w = uniformize<L>(group_broadcast<L>(ww, leader));
-  }
-  bool fresh = true;
-  while (w < games_total) {
-    if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
-      const int i = w / p.n_games;
-      const int g = w - i * p.n_games;
-      kind = uniformize<L>(p.kind[w]);
-      gr = genomes + (long)genome_row(p, i) * p.gstride;
-      load_net<L, U, O, WT>(nr, gr, H, b, lig);
-      if (kind == kOppNN) {
-        gl = opponents + (long)p.opp[w] * p.ostride;
-        load_net<L, U, O, WT>(nl, gl, H, b, lig);
-      }
-      st.reset(game_seed(p.seed, g), kind == kOppRomCpu);
-      act_r = act_l = timeout = total = frames = 0;
-      fresh = false;
-    }
-    const int s1b = st.s1, s2b = st.s2;
-    const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
-    st.step(act_r, act_l);
-    frames += 1;
-    const int vis = st.vis;
-    const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
-    const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
-    int left = 0, right = 0;
-    if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
-      const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
-      const int kr[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
-      const int kl[6] = {320 - bx2, by2, 320 - lbx2, lby2, lc2, rc2};  // x flipped, main.py:146-147
-      const bool left_nn = kind == kOppNN;
-      int scripted = hardcoded(by2, lc2);
-      if (kind == kOppScore && st.s1 > st.s2) scripted = 0;
-#ifdef PG_ABLATE_NN  // timing-only build: scripted paddles on both sides, no network
-      const int2 d = make_int2(hardcoded(by2, rc2), scripted);
-#else
-      const int2 d = decide<L, U, O, WT>(nr, gr, kr, nl, gl, kl, left_nn, scripted, H, b, lds, lig, slow);
-#endif
-      right = d.x;
-      left = d.y;
-      c_fwd += left_nn ? 2 : 1;
-    }
-    act_l = uniformize<L>(clamp_action(lc2, left));
-    act_r = uniformize<L>(clamp_action(rc2, right));
-    if (p.trace && w < p.trace_games && frames <= p.trace_cap && lig == 0)
-      p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
-    if (frames > 1) {
-      if (st.s1 == s1b && st.s2 == s2b) {
-        timeout += 1;
-      } else {
-        total += timeout;
-        timeout = 0;
-      }
-    }
-    if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) {
-      if (lig == 0) finish_game(p, w, st, frames, total);
-      c_steps += frames;
-      c_games += 1;
-      int ww = 0;
-      if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
-      w = uniformize<L>(group_broadcast<L>(ww, leader));
-      fresh = true;
-    }
-  }
-  if (p.counters && lig == 0 && c_games) {
-    atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)c_steps);
-    atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);
-    atomicAdd((unsigned long long *)&p.counters[2], (unsigned long long)slow);
-    atomicAdd((unsigned long long *)&p.counters[3], (unsigned long long)c_games);
-  }
-}
-
-
-#endif  // PG_WITH_EXPERIMENTAL
 // --------------------------------------------------------------- decide ----
 // k_service's decision cascade on given inputs (pg_decide): the split layout's
 // f32 pass (load_net_pk / partial_pk / group_sum<HL>, the same z and bound e a
@@ -773,21 +670,6 @@ static ResidentChoice choose_resident(int H, int requested_L) {
   return {0, 0};
 }
 
-#ifdef PG_WITH_EXPERIMENTAL
-template <int L, int U, int O, typename WT>
-static int32_t launch_resident(const EvalParams &p, hipStream_t s) {
-  constexpr int GPB = 256 / L;
-  const size_t lds = (size_t)GPB * f64_lds_doubles(p.nodes[1], O) * sizeof(double);
-  const int want = (p.total + GPB - 1) / GPB;
-  const int cap = num_cus() * 8;
-  const int grid = want < cap ? want : cap;
-  if (grid <= 0) return PG_OK;
-  hipLaunchKernelGGL((k_resident<L, U, O, WT>), dim3(grid), dim3(256), lds, s, p);
-  PG_HIP(hipGetLastError());
-  return PG_OK;
-}
-
-#endif  // PG_WITH_EXPERIMENTAL
 
 // split layout for hidden width H: L lanes per game (L/2 per network).  Fewer
 // lanes per game means more games per wave, so the replicated scalar work of
@@ -820,29 +702,6 @@ static int32_t launch_service_any(const EvalParams &p, int L, int O, hipStream_t
 #endif
 }
 
-#ifdef PG_WITH_EXPERIMENTAL
-template <int L, int U, typename WT>
-static int32_t launch_resident_o(const EvalParams &p, int O, hipStream_t s) {
-  switch (O) {
-    case 2: return launch_resident<L, U, 2, WT>(p, s);
-    case 3: return launch_resident<L, U, 3, WT>(p, s);
-    case 4: return launch_resident<L, U, 4, WT>(p, s);
-  }
-  return fail(PG_ERR_UNSUPPORTED, "resident kernel supports 2..4 outputs, got %d", O);
-}
-
-template <typename WT>
-static int32_t launch_resident_any(const EvalParams &p, ResidentChoice c, int O, hipStream_t s) {
-#define PG_RES(LL, UU) \
-  if (c.L == LL && c.U == UU) return launch_resident_o<LL, UU, WT>(p, O, s);
-#ifndef PG_DEV_MIN
-  PG_RES(4, 1) PG_RES(8, 1) PG_RES(16, 1) PG_RES(32, 1) PG_RES(64, 1)
-  PG_RES(16, 2) PG_RES(32, 2) PG_RES(64, 2) PG_RES(16, 4) PG_RES(32, 4) PG_RES(64, 4)
-#endif
-#undef PG_RES
-  return fail(PG_ERR_UNSUPPORTED, "no resident kernel for L=%d U=%d", c.L, c.U);
-}
-#endif  // PG_WITH_EXPERIMENTAL
 
 template <int L, int U, int O, typename WT>
 static int32_t launch_fwd_resident(const FwdParams &p, hipStream_t s) {
@@ -886,13 +745,7 @@ extern "C" {
 
 const char *pg_version(void) { return PG_VERSION_STRING; }
 int32_t pg_abi_version(void) { return PG_ABI_VERSION; }
-int32_t pg_build_flags(void) {
-#ifdef PG_WITH_EXPERIMENTAL
-  return 1;
-#else
-  return 0;
-#endif
-}
+int32_t pg_build_flags(void) { return 0; }
 const char *pg_last_error(void) { return g_last_error.c_str(); }
 
 int32_t pg_device_count(void) {
@@ -933,9 +786,6 @@ size_t pg_eval_workspace_bytes(const pg_eval_args *a) {
   if (!a) return n;
   const int kernel = resolve_kernel(a);
   if (kernel == PG_KERNEL_SPLIT) n += split_records_bytes(a);
-#ifdef PG_WITH_EXPERIMENTAL
-  if (kernel == PG_KERNEL_STAGED) n += (staged_workspace_bytes(a) + 255) / 256 * 256;
-#endif
   if (kernel == PG_KERNEL_WIDE && wide_shape_ok(a->net, a->n_games)) n += (wide_workspace_bytes(a) + 255) / 256 * 256;
   return n;
 }
@@ -953,7 +803,11 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   if (rc != PG_OK) return rc;
   if (a->n_genomes < 0) return fail(PG_ERR_INVALID, "n_genomes=%d < 0", a->n_genomes);
   if (a->n_games < 1 || a->n_games > 64) return fail(PG_ERR_INVALID, "n_games=%d not in [1, 64]", a->n_games);
-  if (a->n_genomes == 0) return PG_OK;
+  if (a->horizon < 0) return fail(PG_ERR_INVALID, "horizon=%d < 0", a->horizon);
+  if (a->n_genomes == 0) {  // nothing to play (e.g. an empty shard); the counters still read zero
+    if (a->counters) PG_HIP(hipMemsetAsync(a->counters, 0, 16 * sizeof(uint64_t), (hipStream_t)stream));
+    return PG_OK;
+  }
   const long total = (long)a->n_genomes * a->n_games;
   if (total > 0x7fffffffL) return fail(PG_ERR_INVALID, "too many games (%ld)", total);
   const int G = gene_count(a->net);
@@ -969,6 +823,9 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   if (a->trace && (a->trace_games < 0 || a->trace_cap < 1))
     return fail(PG_ERR_INVALID, "trace needs trace_games >= 0 and trace_cap >= 1");
   if (a->prep < PG_PREP_ALL || a->prep > PG_PREP_REST) return fail(PG_ERR_INVALID, "prep=%d", a->prep);
+  if (a->horizon > 0 && a->trace) return fail(PG_ERR_INVALID, "horizon mode runs untraced (trace must be NULL)");
+  if (a->horizon > 0 && resolve_kernel(a) != PG_KERNEL_SPLIT)
+    return fail(PG_ERR_UNSUPPORTED, "horizon mode runs on the SPLIT kernel ([6, H<=64, 3], certified)");
   const size_t need = pg_eval_workspace_bytes(a);
   if (!a->workspace || a->workspace_bytes < need)
     return fail(PG_ERR_INVALID, "workspace of %zu bytes required (got %zu)", need, a->workspace_bytes);
@@ -1008,6 +865,7 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   p.max_width = max_width(a->net);
 
   p.prep = a->prep;
+  p.horizon = a->horizon;
   const int kernel = resolve_kernel(a);
   if (kernel != PG_KERNEL_SPLIT) {
     if (a->prep == PG_PREP_GENOMES) return PG_OK;  // no records outside the split kernel
@@ -1033,29 +891,9 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
     if (rc != PG_OK) return rc;
     if (a->prep == PG_PREP_GENOMES) return PG_OK;  // records only: no games, no fitness
   } else if (kernel == PG_KERNEL_RESIDENT || kernel == PG_KERNEL_STAGED) {
-#ifndef PG_WITH_EXPERIMENTAL
-    return fail(PG_ERR_UNSUPPORTED, "the %s kernel is an experimental layout, not in the product library "
-                "(build with PG_EXPERIMENTAL=1)", kernel == PG_KERNEL_RESIDENT ? "resident" : "staged");
-#else
-    if (kernel == PG_KERNEL_STAGED) {
-      if (!staged_shape_ok(a->net)) return fail(PG_ERR_UNSUPPORTED, "staged kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
-      if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "staged kernel is the certified-precision path");
-      // k_prep_rows prepares the opponent records from the opponents table; a
-      // network game's opp row would otherwise index unprepared records
-      if (!a->opponents || a->n_opponents <= 0)
-        return fail(PG_ERR_UNSUPPORTED, "staged kernel needs an opponents table (use the split kernel)");
-      rc = launch_staged(p, a, (char *)a->workspace + eval_base_workspace(a), s);
-      if (rc != PG_OK) return rc;
-    } else {
-    if (!res_ok) return fail(PG_ERR_UNSUPPORTED, "resident kernel needs NETWORK_SHAPE [6, H<=256, 2..4]");
-    if (a->precision != PG_PREC_CERTIFIED) return fail(PG_ERR_UNSUPPORTED, "resident kernel is the certified-precision path");
-    const ResidentChoice c = choose_resident(a->net.nodes[1], a->group_lanes);
-    if (c.L == 0) return fail(PG_ERR_UNSUPPORTED, "no resident kernel for H=%d group_lanes=%d", a->net.nodes[1], a->group_lanes);
-    rc = a->net.dtype == PG_F64 ? launch_resident_any<double>(p, c, a->net.nodes[2], s)
-                                : launch_resident_any<float>(p, c, a->net.nodes[2], s);
-    if (rc != PG_OK) return rc;
-    }
-#endif
+    // retired layouts (correct, measured slower than SPLIT; removed in round 4)
+    return fail(PG_ERR_UNSUPPORTED, "the %s kernel was retired (DESIGN 4.1b-c); use SPLIT",
+                kernel == PG_KERNEL_RESIDENT ? "resident" : "staged");
   } else if (kernel == PG_KERNEL_GENERAL) {
     const size_t lds = 2 * (size_t)(p.max_width + 1) * sizeof(double);
     if (lds > 160 * 1024) return fail(PG_ERR_UNSUPPORTED, "layer width %d too large for LDS", p.max_width);

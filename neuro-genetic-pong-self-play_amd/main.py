@@ -181,11 +181,13 @@ def get_actions(ball_location, last_ball_location, left_location, left_model, ri
     ball and a visible paddle decide through the model (the left player sees
     the field x-flipped); a missing paddle keeps a random action; no ball, no
     move.  Each model call is one device forward (numpy_nn.NeuralNetwork.run)."""
+    # both defaults drawn first, as the reference does on every frame (main.py:137-138):
+    # numpy's global RNG stream stays the reference's, ball or no ball
+    left_action = utils.get_random_action(ALL_ACTIONS)  # noqa: F405
+    right_action = utils.get_random_action(ALL_ACTIONS)  # noqa: F405
     if ball_location is None:
         return [0, 0], [0, 0]
     last = ball_location if last_ball_location is None else last_ball_location
-    left_action = utils.get_random_action(ALL_ACTIONS)  # noqa: F405
-    right_action = utils.get_random_action(ALL_ACTIONS)  # noqa: F405
     if left_location is not None:
         def flip(loc):  # [row, column] with the column mirrored
             return [loc[0], GAME_WIDTH - loc[1]]  # noqa: F405

@@ -16,7 +16,7 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 7
+PG_ABI_VERSION = 8
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -55,7 +55,7 @@ class PgEvalArgs(ctypes.Structure):
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
         ("hard_log", _vp), ("hard_cap", ctypes.c_int32), ("genome_rows", _vp),
         ("n_active", _vp),
-        ("prep", ctypes.c_int32),
+        ("prep", ctypes.c_int32), ("horizon", ctypes.c_int32),
     ]
 
 
@@ -245,11 +245,6 @@ def lib() -> ctypes.CDLL:
                 raise RuntimeError(f"{LIB_PATH}: ABI {L.pg_abi_version()} != {PG_ABI_VERSION}")
             _lib = L
     return _lib
-
-
-def experimental() -> bool:
-    """Whether this library has the experimental layouts (k_resident, k_staged)."""
-    return bool(lib().pg_build_flags() & 1)
 
 
 def check(func: str, rc: int) -> None:

@@ -10,22 +10,18 @@ from ._lib import LIB_PATH, PKG_DIR, REPO_DIR
 
 CSRC = os.path.join(PKG_DIR, "csrc")
 # one translation unit per kernel family, compiled in parallel and linked into one .so
-# PG_EXPERIMENTAL=1 also builds the alternative evaluation layouts k_resident
-# and k_staged (correct, measured slower than k_service), which
-# the product library leaves out; their GPU tests skip without them.
-EXPERIMENTAL = os.environ.get("PG_EXPERIMENTAL") == "1"
 SOURCES = [os.path.join(CSRC, f) for f in ("pong_ga.hip", "pg_wide.hip", "pg_pixels.hip", "pg_service_more.hip",
-                                           "pg_hof.hip", "pg_gen.hip") + (("pg_staged.hip",) if EXPERIMENTAL else ())]
-DEPS = SOURCES + [os.path.join(CSRC, "pg_staged.hip")] + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp", "pg_cascade.hpp", "pg_service.hpp")] + [
+                                           "pg_hof.hip", "pg_gen.hip")]
+DEPS = SOURCES + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp", "pg_cascade.hpp", "pg_service.hpp")] + [
     os.path.join(REPO_DIR, "include", "pong_ga.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # per-source flags: the iterative ILP machine scheduler makes k_service's frame
 # loop ~5 % faster on the bench than the default (13.57 vs 14.3 ms per launch;
 # max-ilp 13.85; iterative-minreg +9 %, max-memory-clause +4 %,
 # iterative-maxocc +37 %, the newer RP trackers +6 %, -O2 +3 % slower)
-# (pg_staged.hip and pg_service_more.hip keep the default scheduler: iterative-ilp
-# crashes the register allocator on k_prep_rows and on some small k_service
-# layouts in this compiler, so pong_ga.hip instantiates only the bench layout)
+# (pg_service_more.hip keeps the default scheduler: iterative-ilp crashes the
+# register allocator on some small k_service layouts in this compiler, so
+# pong_ga.hip instantiates only the bench layout)
 SOURCE_FLAGS = {"pong_ga.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 ARCH = os.environ.get("PG_OFFLOAD_ARCH", "gfx950")
 
@@ -42,8 +38,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB_PATH  # a prebuilt variant (tools/build_variant.py): never rebuilt from the product sources
     if not force and not needs_build():
         return LIB_PATH
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off"] + (
-        ["-DPG_WITH_EXPERIMENTAL"] if EXPERIMENTAL else []) + [
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off"] + [
              # no SLP packing of independent f32 adds into v_pk_add_f32: it breaks the
              # DPP-fused reductions into mov_dpp + pk_add pairs (measured -5 %)
              "-fno-slp-vectorize", "-fPIC",

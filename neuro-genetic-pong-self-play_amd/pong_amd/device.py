@@ -16,8 +16,8 @@ from . import _lib as L
 
 PRECISIONS = {"certified": L.PG_PREC_CERTIFIED, "f64": L.PG_PREC_F64}
 PREPS = {"all": L.PG_PREP_ALL, "genomes": L.PG_PREP_GENOMES, "rest": L.PG_PREP_REST}
-KERNELS = {"auto": L.PG_KERNEL_AUTO, "general": L.PG_KERNEL_GENERAL, "resident": L.PG_KERNEL_RESIDENT,
-           "split": L.PG_KERNEL_SPLIT, "wide": L.PG_KERNEL_WIDE, "staged": L.PG_KERNEL_STAGED}
+KERNELS = {"auto": L.PG_KERNEL_AUTO, "general": L.PG_KERNEL_GENERAL, "split": L.PG_KERNEL_SPLIT,
+           "wide": L.PG_KERNEL_WIDE}
 DTYPES = {torch.float32: L.PG_F32, torch.float64: L.PG_F64}
 
 
@@ -67,7 +67,7 @@ class Evaluator:
     """Population evaluator for one NETWORK_SHAPE on one device."""
 
     def __init__(self, nodes, bias=True, dtype=torch.float64, device=None, n_games=6,
-                 precision="certified", kernel="auto", group_lanes=0, seed=0):
+                 precision="certified", kernel="auto", group_lanes=0, seed=0, horizon=0):
         if not torch.cuda.is_available():
             raise RuntimeError("pong_amd.Evaluator needs a HIP device (no CPU fallback)")
         L.lib()
@@ -80,9 +80,13 @@ class Evaluator:
         self.kernel = kernel
         self.group_lanes = int(group_lanes)
         self.seed = int(seed)
+        # pg_eval_args.horizon: 0 = evaluate()'s episodes; T > 0 = SURVEY 8(d)'s
+        # fixed-horizon measurement mode (T frames per game slot, auto-reset)
+        self.horizon = int(horizon)
         self.genes = gene_count(self.nodes, self.bias)
         self.net = L.make_net(self.nodes, self.bias, DTYPES[dtype])
         self._ws = None
+        self._prep_key = self._prep_ws = None  # what the last prep="genomes" call left in the workspace
 
     # ------------------------------------------------------------ schedules
     def selfplay_schedule(self, n: int, n_opponents: int, offset: int = 0):
@@ -107,7 +111,7 @@ class Evaluator:
                  out: Optional[EvalResult] = None, precision: Optional[str] = None,
                  kernel: Optional[str] = None, group_lanes: Optional[int] = None, validate: bool = True,
                  hard_log: Optional[torch.Tensor] = None, rows: Optional[torch.Tensor] = None,
-                 n_active: Optional[torch.Tensor] = None, prep: str = "all"):
+                 n_active: Optional[torch.Tensor] = None, prep: str = "all", horizon: Optional[int] = None):
         """Run every genome's games to termination; returns (EvalResult, trace or None).
 
         ``validate`` checks the schedule's opponent rows on the host first (one
@@ -123,6 +127,9 @@ class Evaluator:
         plays after such a call with the same genomes, rows, n_active and
         evaluator (its workspace holds the records), preparing the opponents'
         records first.
+        ``horizon`` (pg_eval_args.horizon, default ``self.horizon``): T > 0 runs
+        every game slot for exactly T frames with auto-reset (rewards = the
+        completed episodes' sum, total_frames = their count; see pong_ga.h).
         """
         dev = self.device
         n = genomes.shape[0] if rows is None else rows.shape[0]
@@ -192,13 +199,29 @@ class Evaluator:
                 raise ValueError("hard_log must be [cap, 8] int32")
             a.hard_log, a.hard_cap = _ptr(hard_log), hard_log.shape[0]
         a.prep = PREPS[prep]
+        if prep == "rest" and n and self._prep_key != self._prep_of(genomes, rows, n_active, n):
+            # pg_eval_args.prep: a "rest" call plays the genome records a "genomes"
+            # call left in this evaluator's workspace -- they must be these genomes'
+            raise ValueError("prep='rest' needs a preceding prep='genomes' call with the same genomes, rows, "
+                             "n_active and row count on this evaluator")
+        a.horizon = self.horizon if horizon is None else int(horizon)
         a.kernel = KERNELS[kernel or self.kernel]
         a.group_lanes = self.group_lanes if group_lanes is None else int(group_lanes)
         ws = self._workspace(a)
         a.workspace, a.workspace_bytes = _ptr(ws), ws.numel()
+        if prep == "rest" and n and self._prep_ws != ws.data_ptr():
+            raise ValueError("prep='rest': the workspace holding the genome records was reallocated")
         with torch.cuda.device(dev):
             L.check("pg_eval_population", L.lib().pg_eval_population(ctypes.byref(a), _stream(dev)))
+        # the genome records in the workspace now belong to this call's genomes (or to no one)
+        self._prep_key = self._prep_of(genomes, rows, n_active, n) if prep == "genomes" else None
+        self._prep_ws = ws.data_ptr() if prep == "genomes" else None
         return out, trace
+
+    @staticmethod
+    def _prep_of(genomes, rows, n_active, n):
+        return (genomes.data_ptr(), genomes.stride(0), None if rows is None else rows.data_ptr(),
+                None if n_active is None else n_active.data_ptr(), int(n))
 
     # -------------------------------------------------------------- forward
     def forward(self, genomes: torch.Tensor, x: torch.Tensor, genome_index: Optional[torch.Tensor] = None,

@@ -175,6 +175,8 @@ class DeviceGA:
             raise ValueError("hall-of-fame members must be ordered best first")
         if genomes is not None:
             self.store[:n] = genomes.to(device=self.device, dtype=self.dtype)
+        # a prepared next generation (_early_prep) assumed the old hall's size
+        self._next = None
         self.hof_n = n
         self._hof_fit_host = fit.copy()
         if n:

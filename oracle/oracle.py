@@ -77,6 +77,13 @@ def lib() -> ctypes.CDLL:
         L.or_play_game.argtypes = [dp, ctypes.POINTER(OrNet), ctypes.c_int, dp, ctypes.c_double,
                                    ctypes.c_uint64, ctypes.POINTER(OrGameResult),
                                    ctypes.POINTER(ctypes.c_uint8), ctypes.c_int]
+        L.or_play_slot.argtypes = [dp, ctypes.POINTER(OrNet), ctypes.c_int, dp, ctypes.c_double,
+                                   ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(OrGameResult),
+                                   ctypes.POINTER(ctypes.c_uint8), ctypes.c_int]
+        L.or_eval_population_h.restype = ctypes.c_int
+        L.or_eval_population_h.argtypes = [
+            ctypes.c_int, ctypes.c_int, dp, ctypes.c_int64, dp, ctypes.c_int64, ip, ip, dp,
+            ctypes.POINTER(OrNet), ctypes.c_uint64, ctypes.c_int, dp, dp, ip, ip, dp, ip, ctypes.c_int]
         L.or_eval_population.restype = ctypes.c_int
         L.or_eval_population.argtypes = [
             ctypes.c_int, ctypes.c_int, dp, ctypes.c_int64, dp, ctypes.c_int64, ip, ip, dp,
@@ -164,13 +171,15 @@ class Env:
         return {name: getattr(self.state, name) for name, _ in OrState._fields_}
 
 
-def play_game(genes, nodes, opp_kind, opp_genes=None, mult=1.0, seed=0, bias=True, trace_cap=0):
+def play_game(genes, nodes, opp_kind, opp_genes=None, mult=1.0, seed=0, bias=True, trace_cap=0, horizon=0):
+    """One game slot (or_play_slot): a perform_episode, or with ``horizon`` > 0
+    the fixed-horizon mode (T frames, auto-reset; pong_ga.h pg_eval_args.horizon)."""
     net = Net(nodes, bias)
     g = np.ascontiguousarray(genes, dtype=np.float64)
     og = np.ascontiguousarray(opp_genes, dtype=np.float64) if opp_genes is not None else None
     res = OrGameResult()
     trace = (ctypes.c_uint8 * max(trace_cap, 1))()
-    lib().or_play_game(_dp(g), net.ref, int(opp_kind), _dp(og), float(mult), seed,
+    lib().or_play_slot(_dp(g), net.ref, int(opp_kind), _dp(og), float(mult), seed, int(horizon),
                        ctypes.byref(res), trace if trace_cap else None, int(trace_cap))
     out = {k: getattr(res, k) for k, _ in OrGameResult._fields_}
     if trace_cap:
@@ -179,8 +188,9 @@ def play_game(genes, nodes, opp_kind, opp_genes=None, mult=1.0, seed=0, bias=Tru
 
 
 def eval_population(genomes, nodes, kind, opp_index, mult, opponents=None, bias=True,
-                    base_seed=0, n_threads=0):
-    """Whole-population evaluate(): returns a dict of numpy arrays."""
+                    base_seed=0, n_threads=0, horizon=0):
+    """Whole-population evaluate(): returns a dict of numpy arrays (``horizon`` > 0:
+    every game slot in the fixed-horizon mode, or_eval_population_h)."""
     net = Net(nodes, bias)
     G = np.ascontiguousarray(genomes, dtype=np.float64)
     n = G.shape[0]
@@ -197,9 +207,9 @@ def eval_population(genomes, nodes, kind, opp_index, mult, opponents=None, bias=
     frames = np.zeros((n, n_games), np.int32)
     total = np.zeros((n, n_games), np.float64)
     status = np.zeros(n, np.int32)
-    first_err = lib().or_eval_population(
+    first_err = lib().or_eval_population_h(
         n, n_games, _dp(G), G.shape[1] if n else 0, _dp(O), O.shape[1], _ip(kind), _ip(opp_index),
-        _dp(mult), net.ref, base_seed, _dp(fitness), _dp(rewards), _ip(scores), _ip(frames),
+        _dp(mult), net.ref, base_seed, int(horizon), _dp(fitness), _dp(rewards), _ip(scores), _ip(frames),
         _dp(total), _ip(status), int(n_threads))
     return {"fitness": fitness, "rewards": rewards, "scores": scores, "frames": frames,
             "total_frames": total, "status": status, "first_error": first_err}

@@ -268,9 +268,29 @@ static int clamp_action(int c2, int code) { /* keep_within_game_bounds_please ut
   return code;
 }
 
-void or_play_game(const double *genes, const or_net *net, int opp_kind,
-                  const double *opp_genes, double mult, uint64_t game_seed,
-                  or_game_result *out, uint8_t *trace, int trace_cap) {
+/* perform_episode's return value (main.py:108-112, calculate_reward utils.py:104-109) */
+static double episode_reward(const or_pong_state *s, double total, double mult, int *zero_division) {
+  *zero_division = 0;
+  if (s->score1 == s->score2) return 0.0; /* main.py:109-110 */
+  if (total == 0.0) {
+    *zero_division = 1; /* utils.py:106-108 would raise ZeroDivisionError */
+    return NAN;
+  }
+  double diff = (double)(s->score2 - s->score1);
+  double scaled = total / 100.0;
+  double bonus = (double)s->score2 * mult;
+  return (diff + bonus) / scaled;
+}
+
+/* One game slot.  horizon <= 0: one perform_episode (main.py:69-112).
+ * horizon T > 0: SURVEY 8(d)'s fixed-horizon measurement mode (pong_ga.h
+ * pg_eval_args.horizon): exactly T frames; an episode that terminates before
+ * frame T is scored and the env auto-resets (the serve sequence continues:
+ * the point counter is kept), the partial last episode is dropped.  Result:
+ * reward = the completed episodes' rewards summed in order, score1/score2 =
+ * the points of all episodes, frames = T, total_frames = completed episodes. */
+void or_play_slot(const double *genes, const or_net *net, int opp_kind, const double *opp_genes, double mult,
+                  uint64_t game_seed, int horizon, or_game_result *out, uint8_t *trace, int trace_cap) {
   or_pong_state s;
   or_env_reset(&s, game_seed, opp_kind == OR_OPP_ROM_CPU);
   int act_r = 0, act_l = 0;
@@ -278,6 +298,8 @@ void or_play_game(const double *genes, const or_net *net, int opp_kind,
   int have_last_score = 0, last1 = 0, last2 = 0;
   int have_last_ball = 0, lby2 = 0, lbx2 = 0;
   int frames = 0;
+  double h_reward = 0.0;
+  int h_eps = 0, h_s1 = 0, h_s2 = 0, h_zd = 0;
   for (;;) {
     or_env_step(&s, act_r == 1, act_r == 2, act_l == 1, act_l == 2);
     frames += 1;
@@ -334,27 +356,55 @@ void or_play_game(const double *genes, const or_net *net, int opp_kind,
     have_last_score = 1;
     last1 = s.score1;
     last2 = s.score2;
-    if (s.score1 >= OR_WIN_SCORE || s.score2 >= OR_WIN_SCORE) break;
-    if (or_env_done(&s)) break;
-    if (timeout > (double)OR_TIMEOUT_THRESH) break;
+    /* termination main.py:102-107 */
+    const int ep_end = s.score1 >= OR_WIN_SCORE || s.score2 >= OR_WIN_SCORE || or_env_done(&s) ||
+                       timeout > (double)OR_TIMEOUT_THRESH;
+    if (horizon <= 0) {
+      if (ep_end) break;
+      continue;
+    }
+    if (ep_end) { /* score the episode, then auto-reset the slot */
+      int zd = 0;
+      h_reward += episode_reward(&s, total, mult, &zd);
+      h_zd |= zd;
+      h_eps += 1;
+      h_s1 += s.score1;
+      h_s2 += s.score2;
+      if (frames >= horizon) break;
+      const int point = s.point;
+      or_env_reset(&s, game_seed, opp_kind == OR_OPP_ROM_CPU);
+      s.point = point;
+      act_r = act_l = 0;
+      timeout = total = 0.0;
+      have_last_score = have_last_ball = 0;
+      continue;
+    }
+    if (frames >= horizon) { /* the partial last episode: its points only */
+      h_s1 += s.score1;
+      h_s2 += s.score2;
+      break;
+    }
+  }
+  out->slow_decisions = 0;
+  out->frames = frames;
+  if (horizon > 0) {
+    out->score1 = h_s1;
+    out->score2 = h_s2;
+    out->total_frames = (double)h_eps;
+    out->reward = h_reward;
+    out->zero_division = h_zd;
+    return;
   }
   out->score1 = s.score1;
   out->score2 = s.score2;
-  out->frames = frames;
   out->total_frames = total;
-  out->zero_division = 0;
-  out->slow_decisions = 0;
-  if (s.score1 == s.score2) {
-    out->reward = 0.0; /* main.py:109-110 */
-  } else if (total == 0.0) {
-    out->zero_division = 1; /* utils.py:106-108 would raise ZeroDivisionError */
-    out->reward = NAN;
-  } else { /* calculate_reward utils.py:104-109 */
-    double diff = (double)(s.score2 - s.score1);
-    double scaled = total / 100.0;
-    double bonus = (double)s.score2 * mult;
-    out->reward = (diff + bonus) / scaled;
-  }
+  out->reward = episode_reward(&s, total, mult, &out->zero_division);
+}
+
+void or_play_game(const double *genes, const or_net *net, int opp_kind,
+                  const double *opp_genes, double mult, uint64_t game_seed,
+                  or_game_result *out, uint8_t *trace, int trace_cap) {
+  or_play_slot(genes, net, opp_kind, opp_genes, mult, game_seed, 0, out, trace, trace_cap);
 }
 
 int or_eval_population(int n, int n_games, const double *genomes, int64_t stride,
@@ -364,6 +414,17 @@ int or_eval_population(int n, int n_games, const double *genomes, int64_t stride
                        double *fitness, double *rewards, int32_t *scores,
                        int32_t *frames, double *total_frames, int32_t *status,
                        int n_threads) {
+  return or_eval_population_h(n, n_games, genomes, stride, opponents, opp_stride, kind, opp_index, mult, net,
+                              base_seed, 0, fitness, rewards, scores, frames, total_frames, status, n_threads);
+}
+
+int or_eval_population_h(int n, int n_games, const double *genomes, int64_t stride,
+                         const double *opponents, int64_t opp_stride,
+                         const int32_t *kind, const int32_t *opp_index,
+                         const double *mult, const or_net *net, uint64_t base_seed, int horizon,
+                         double *fitness, double *rewards, int32_t *scores,
+                         int32_t *frames, double *total_frames, int32_t *status,
+                         int n_threads) {
   int first_err = 0;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : 1) if (n_threads > 1)
@@ -376,8 +437,8 @@ int or_eval_population(int n, int n_games, const double *genomes, int64_t stride
       const double *opp = NULL;
       if (kind[k] == OR_OPP_NN) opp = opponents + (long)opp_index[k] * opp_stride;
       or_game_result r;
-      or_play_game(genomes + (long)i * stride, net, kind[k], opp, mult[k],
-                   or_game_seed(base_seed, g), &r, NULL, 0);
+      or_play_slot(genomes + (long)i * stride, net, kind[k], opp, mult[k],
+                   or_game_seed(base_seed, g), horizon, &r, NULL, 0);
       if (rewards) rewards[k] = r.reward;
       if (scores) {
         scores[2 * k] = r.score1;

@@ -110,6 +110,11 @@ void or_play_game(const double *genes, const or_net *net, int opp_kind,
                   const double *opp_genes, double mult, uint64_t game_seed,
                   or_game_result *out, uint8_t *trace, int trace_cap);
 
+/* One game slot: horizon <= 0 is or_play_game; horizon T > 0 the fixed-horizon
+ * measurement mode of pg_eval_args.horizon (T frames, auto-reset, see there). */
+void or_play_slot(const double *genes, const or_net *net, int opp_kind, const double *opp_genes, double mult,
+                  uint64_t game_seed, int horizon, or_game_result *out, uint8_t *trace, int trace_cap);
+
 /* A whole population: games per genome = n_games; kind/opp/mult are
  * [n, n_games]; opponents[opp_index * stride ...]; fitness = evaluate().
  * n_threads <= 0 means serial.  Returns 0, or the 1-based index of the first
@@ -121,6 +126,14 @@ int or_eval_population(int n, int n_games, const double *genomes, int64_t stride
                        double *fitness, double *rewards, int32_t *scores,
                        int32_t *frames, double *total_frames, int32_t *status,
                        int n_threads);
+/* The same with every game slot in the fixed-horizon mode (horizon > 0). */
+int or_eval_population_h(int n, int n_games, const double *genomes, int64_t stride,
+                         const double *opponents, int64_t opp_stride,
+                         const int32_t *kind, const int32_t *opp_index,
+                         const double *mult, const or_net *net, uint64_t base_seed, int horizon,
+                         double *fitness, double *rewards, int32_t *scores,
+                         int32_t *frames, double *total_frames, int32_t *status,
+                         int n_threads);
 
 /* ---- pixel path (utils.py:14-19, 60-68; the build's frame of its state) ---- */
 #define OR_FRAME_BYTES (210 * 160 * 3)

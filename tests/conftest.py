@@ -51,10 +51,3 @@ def gpu():
     B.build()
     return torch.device("cuda", 0)
 
-
-def need_experimental():
-    """Skip: k_resident / k_staged are alternative layouts kept out of the
-    product library; PG_EXPERIMENTAL=1 builds them in."""
-    from pong_amd import _lib
-    if not _lib.experimental():
-        pytest.skip("experimental evaluation layouts not built (PG_EXPERIMENTAL=1)")

@@ -73,6 +73,10 @@ def test_validation_errors_without_gpu(lib):
     a.genome_stride = 3  # < 20 genes
     assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_ERR_INVALID
     assert b"genome_stride" in lib.pg_last_error()
+    a.horizon = -1  # the fixed-horizon mode: T >= 0
+    assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_ERR_INVALID
+    assert b"horizon" in lib.pg_last_error()
+    a.horizon = 0
     bad = _lib.make_net([6, 2, 2])
     bad.n_nodes = 1
     assert lib.pg_gene_count(ctypes.byref(bad)) == _lib.PG_ERR_INVALID

@@ -164,9 +164,7 @@ def test_eval_matches_oracle(gpu, oracle, shape, dist):
     # simulated env steps + periodic-rally frames not simulated = the episodes' frames
     assert int(res.counters[0]) + int(res.counters[8]) + int(res.counters[12]) == int(ref["frames"].sum())
     if len(shape) == 3:  # the other kernels must agree too
-        from pong_amd import _lib
-        others = (("general", "f64"),) + ((("resident", "certified"),) if _lib.experimental() else ())
-        for kernel, precision in others:
+        for kernel, precision in (("general", "f64"),):
             res2, _ = ev.evaluate(_dev_genomes(genomes, gpu), torch.tensor(kinds, device=gpu),
                                   torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
                                   opponents=_dev_genomes(opponents, gpu), kernel=kernel, precision=precision)
@@ -174,17 +172,12 @@ def test_eval_matches_oracle(gpu, oracle, shape, dist):
 
 
 @pytest.mark.parametrize("kernel,lanes,hidden", [
-    ("resident", 4, 4), ("resident", 8, 8), ("resident", 16, 16), ("resident", 32, 32), ("resident", 64, 64),
-    ("resident", 16, 64), ("resident", 32, 64), ("resident", 64, 200),
     ("split", 8, 4), ("split", 8, 8), ("split", 8, 64), ("split", 8, 37), ("split", 16, 16), ("split", 16, 64),
     ("split", 16, 40), ("split", 32, 64),
     ("split", 64, 64), ("split", 64, 256), ("split", 32, 50)])
 def test_eval_kernel_layouts(gpu, oracle, kernel, lanes, hidden):
-    """Every lane layout of both register-resident kernels vs the oracle."""
+    """Every lane layout of the split kernel vs the oracle."""
     from pong_amd.device import Evaluator
-    if kernel == "resident":
-        from conftest import need_experimental
-        need_experimental()
     shape = [6, hidden, 3]
     rng = np.random.default_rng(lanes * 1000 + hidden)
     G = _gene_count(shape)
@@ -262,16 +255,13 @@ def test_eval_edge_cases(gpu, oracle):
 
 
 @pytest.mark.parametrize("name", ["episodes.json", "episodes_s3.json"])
-@pytest.mark.parametrize("kernel", ["auto", "staged"])
+@pytest.mark.parametrize("kernel", ["auto"])
 def test_episode_traces_match_reference(gpu, golden, name, kernel):
     """Per-frame actions of the REAL perform_episode (tests/golden/episodes.json;
     episodes_s3.json: N(0, 3) genes, every game slot, long rallies and
     2 000-frame timeouts), traced; then untraced, where the kernels jump over
     periodic rallies -- frames, scores and rewards must not change."""
     from pong_amd.device import Evaluator
-    if kernel == "staged":
-        from conftest import need_experimental
-        need_experimental()
     eps = golden(name)
     for ep in eps:
         shape = ep["shape"]
@@ -336,3 +326,54 @@ def test_full_size_properties(gpu, oracle):
                                  mult[sel].cpu().numpy(), opponents=opponents.cpu().numpy(), n_threads=8)
     np.testing.assert_array_equal(r1.fitness[sel].cpu().numpy(), ref["fitness"])
     np.testing.assert_array_equal(r1.frames[sel].cpu().numpy(), ref["frames"])
+
+
+# ------------------------------------------------- fixed-horizon mode (8d)
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("T", [1, 37, 1000])
+def test_horizon_matches_oracle(gpu, oracle, dtype, T):
+    """pg_eval_args.horizon: every game slot runs exactly T frames with
+    auto-reset; k_service (its horizon instance) equals the oracle's
+    or_eval_population_h bit for bit (rewards summed over the completed
+    episodes, every episode's points, completed-episode counts), in the
+    saturation-heavy N(0, 3) distribution and over every game slot kind."""
+    from pong_amd.device import Evaluator
+    shape = [6, 64, 3]
+    rng = np.random.default_rng(T + (0 if dtype == torch.float64 else 1))
+    G = _gene_count(shape)
+    n, H = 192, 48
+    genomes = rng.standard_normal((n, G)) * 3.0
+    opponents = rng.standard_normal((H, G)) * 3.0
+    if dtype == torch.float32:
+        genomes = genomes.astype(np.float32).astype(np.float64)
+        opponents = opponents.astype(np.float32).astype(np.float64)
+    kinds, opp, mult = _schedule(rng, n, 6, H)
+    kinds[: n // 2] = 3  # half the population in all-network games
+    ev = Evaluator(shape, device=gpu, dtype=dtype, horizon=T)
+    res, _ = ev.evaluate(_dev_genomes(genomes, gpu, dtype), torch.tensor(kinds, device=gpu),
+                         torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
+                         opponents=_dev_genomes(opponents, gpu, dtype))
+    torch.cuda.synchronize()
+    ref = oracle.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents, n_threads=8, horizon=T)
+    _assert_same(res, ref)
+    c = res.counters.cpu().numpy()
+    assert c[0] == n * 6 * T and c[8] == 0 and c[12] == 0, c  # every frame stepped
+    assert (res.frames.cpu().numpy() == T).all()
+    if T == 1000:
+        assert ref["total_frames"].sum() > n * 6  # multi-episode slots were exercised
+
+
+def test_horizon_rejected_where_unsupported(gpu):
+    from pong_amd import _lib
+    from pong_amd.device import Evaluator
+    shape = [6, 16, 3]
+    G = _gene_count(shape)
+    ev = Evaluator(shape, device=gpu, horizon=100)
+    z = torch.zeros((4, 6), dtype=torch.int32, device=gpu)
+    with pytest.raises(_lib.PongGAError):  # only the [6, 33..64, 3] layout has the horizon instance
+        ev.evaluate(torch.zeros((4, G), dtype=torch.float64, device=gpu), z, z,
+                    torch.ones((4, 6), dtype=torch.float64, device=gpu))
+    ev = Evaluator([6, 64, 3], device=gpu, horizon=100)
+    with pytest.raises(_lib.PongGAError):  # and it runs untraced
+        ev.evaluate(torch.zeros((4, _gene_count([6, 64, 3])), dtype=torch.float64, device=gpu), z, z,
+                    torch.ones((4, 6), dtype=torch.float64, device=gpu), trace_games=1, trace_cap=8)
