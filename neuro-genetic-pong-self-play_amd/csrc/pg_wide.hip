@@ -33,8 +33,13 @@ namespace pg {
 constexpr int kWideThreads = 512;  // = max H2: one W2 row per thread
 constexpr int kWideMaxGames = 8;
 
-// W2 tiles: 128 B (K = 128 / sizeof(WT) columns) of every row.
-constexpr int kTileRowBytes = 128;
+// W2 tiles: kTileRowBytes (K = kTileRowBytes / sizeof(WT) columns) of every
+// row, in kPieces 16-B pieces; a wave's piece load is 64 rows x 16 B = 1 KB.
+#ifndef PG_WIDE_TILE_BYTES
+#define PG_WIDE_TILE_BYTES 128
+#endif
+constexpr int kTileRowBytes = PG_WIDE_TILE_BYTES;
+constexpr int kPieces = kTileRowBytes / 16;
 #ifndef PG_WIDE_DEPTH
 #define PG_WIDE_DEPTH 2
 #endif
@@ -71,7 +76,7 @@ constexpr int kStreamPolicy = 2;
 // (W3 staging after layer 2) | h2 [C3][NC] f64 | when they fit: every
 // network's W3 [NG + 1][O][C3] WT.
 constexpr int kOffOut = 1024, kOffCtl = 1536, kOffOrow = 1920, kOffRally = 2048, kOffGames = 2304,
-              kOffH1 = 3328;
+              kOffCount = 3328, kOffH1 = 3584;
 
 // One game's state between frames, kept in LDS by wave 0 (lane c = game c)
 // instead of in VGPRs: every wave of the block carries the frame loop's
@@ -83,7 +88,41 @@ struct WideGame {
   int s1b, s2b, vis, lc2, rc2, left, pad0, pad1;  // this frame's, from phase A to phase E
 };
 static_assert(sizeof(WideGame) == 128, "WideGame: 8 x 16 B");
-static_assert(kOffGames + kWideMaxGames * (int)sizeof(WideGame) <= kOffH1, "LDS carve");
+// whole-record LDS copies as eight 16-B words (an aggregate copy of the
+// struct went through a private-memory temporary)
+__device__ __forceinline__ WideGame wg_load(const WideGame *s) {
+  uint4 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = reinterpret_cast<const uint4 *>(s)[i];
+  WideGame g;
+  __builtin_memcpy(&g, v, sizeof(g));
+  return g;
+}
+__device__ __forceinline__ void wg_store(WideGame *s, const WideGame &g) {
+  uint4 v[8];
+  __builtin_memcpy(v, &g, sizeof(g));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) reinterpret_cast<uint4 *>(s)[i] = v[i];
+}
+
+// The thread index as an opaque value at the top of a loop body: what is
+// derived from it (per-thread LDS and scratch offsets) is then recomputed in
+// the loop instead of hoisted out of it, where ~60 such values had been kept
+// live across layer 2's register ring -- and spilled (round 3: 129 spilled
+// VGPRs; this and the LDS game records: the frame loop spill-free).
+__device__ __forceinline__ int opaque_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+__device__ __forceinline__ int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+v"(z));
+  return z;
+}
+static_assert(kOffGames + kWideMaxGames * (int)sizeof(WideGame) <= kOffCount, "LDS carve");
+// wave 0's per-lane counters (env steps, forwards, games, rally frames skipped), in LDS for the same reason
+static_assert(kOffCount + kWideMaxGames * 4 * 8 <= kOffH1, "LDS carve");
 __host__ __device__ constexpr int align16(int v) { return (v + 15) & ~15; }
 
 __host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b) {
@@ -92,9 +131,9 @@ __host__ __device__ inline int wide_lds_bytes(int NC, int H1, int H2, int b) {
 
 // The tile-major copy of one network's W2 in a block's scratch (written at
 // genome start by wide_prep, read once per frame by layer 2):
-//   tile s < T, piece q < 8, row r < RP: 16 B (E = 16 / sizeof(WT) weights,
-//   columns s*K + q*E ..) at ((s * 8 + q) * RP + r) * 16;
-//   then the tail (columns m2 .. C2-1, at most 3) of row r at (T * 8 * RP + r) * 16
+//   tile s < T, piece q < kPieces, row r < RP: 16 B (E = 16 / sizeof(WT) weights,
+//   columns s*K + q*E ..) at ((s * kPieces + q) * RP + r) * 16;
+//   then the tail (columns m2 .. C2-1, at most 3) of row r at (T * kPieces * RP + r) * 16
 //   (a second such piece block for f64 weights).
 // m2 = C2 - C2 % 4 (blas_dot's block), T = max(1, ceil(m2 / K)), RP = H2 rounded up to 64.
 struct WideLayout {
@@ -106,7 +145,7 @@ __host__ __device__ inline WideLayout wide_layout(int H1, int H2, int b, int wt_
   WideLayout l;
   l.T = m2 > K ? (m2 + K - 1) / K : 1;
   l.RP = (H2 + 63) & ~63;
-  l.net_bytes = (long)(l.T * 8 + (3 * wt_bytes + 15) / 16) * l.RP * 16;
+  l.net_bytes = (long)(l.T * kPieces + (3 * wt_bytes + 15) / 16) * l.RP * 16;
   return l;
 }
 
@@ -137,24 +176,24 @@ __device__ void wide_prep(unsigned char *scratch, const WideLayout lay, const WT
     const WT *row = (n == 0 ? gw2 : ow2 + orow[n - 1]) + (long)t * C2;
     unsigned char *dst = scratch + (long)n * lay.net_bytes + t * 16;
     for (int s = 0; s < lay.T; ++s) {
-      WT v[8][E];
-      const int k0 = s * 8 * E;
-      if (k0 + 8 * E <= m2) {
+      WT v[kPieces][E];
+      const int k0 = s * kPieces * E;
+      if (k0 + kPieces * E <= m2) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
+        for (int q = 0; q < kPieces; ++q)
 #pragma unroll
           for (int e = 0; e < E; ++e) v[q][e] = row[k0 + q * E + e];
       } else {
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
+        for (int q = 0; q < kPieces; ++q)
 #pragma unroll
           for (int e = 0; e < E; ++e) v[q][e] = k0 + q * E + e < m2 ? row[k0 + q * E + e] : WT(0);
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < kPieces; ++q) {
         uint4 u;
         __builtin_memcpy(&u, v[q], 16);
-        *(uint4 *)(dst + (s * 8 + q) * PB) = u;
+        *(uint4 *)(dst + (s * kPieces + q) * PB) = u;
       }
     }
     WT tv[kTP * E];
@@ -164,7 +203,7 @@ __device__ void wide_prep(unsigned char *scratch, const WideLayout lay, const WT
     for (int i = 0; i < kTP; ++i) {
       uint4 u;
       __builtin_memcpy(&u, tv + i * E, 16);
-      *(uint4 *)(dst + (lay.T * 8 + i) * PB) = u;
+      *(uint4 *)(dst + (lay.T * kPieces + i) * PB) = u;
     }
   }
   // the copies are read back through the vector caches by other waves of the block
@@ -204,7 +243,7 @@ __device__ __forceinline__ bool near_tie(const double *v, int O) {
 // (the fields, not the EvalParams: a reference to the kernel's parameter
 // block makes the compiler copy it to private memory, and every field read
 // from there counts as divergent -- layer 2's buffer descriptors included)
-__device__ __noinline__ void log_wide(uint32_t *hard_log, uint64_t *counters, int hard_cap, int row, int is_opp,
+__device__ __forceinline__ void log_wide(uint32_t *hard_log, uint64_t *counters, int hard_cap, int row, int is_opp,
                                       int idx, const double *x) {
   int k[6];
   for (int i = 0; i < 6; ++i) k[i] = (int)rint(x[i] * 320.0);  // the doubled centroids back from k/320
@@ -252,6 +291,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   long long *orow = (long long *)(lds_raw + kOffOrow);  // [NG] opponent row offsets (elements)
   uint64_t *rkey = (uint64_t *)(lds_raw + kOffRally);    // [NG] Brent's saved rally key per game
   WideGame *games = (WideGame *)(lds_raw + kOffGames);    // [NG] the games' states (wave 0)
+  uint64_t *cnt = (uint64_t *)(lds_raw + kOffCount);      // [NG][4] steps, forwards, games, skipped (wave 0)
   int *rat = (int *)(lds_raw + kOffRally + 64), *rspan = (int *)(lds_raw + kOffRally + 96);
   double *h1 = (double *)(lds_raw + kOffH1);            // [C2][NC]
   double *h2 = (double *)(lds_raw + kOffH1 + align16(C2 * NC * 8));  // [C3][NC]
@@ -266,10 +306,12 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   const WT *opponents = (const WT *)p.opponents;
   const int n_games = p.n_games;
   const bool probe = p.wide_probe_k != nullptr;  // pg_wide_decide (n_games = 1)
-  uint64_t c_steps = 0, c_fwd = 0, c_games = 0, c_streams = 0, c_skip = 0;
+  uint64_t c_streams = 0;
+  if (t < NG * 4) cnt[t] = 0;  // (the genome loop's first barrier orders this before any use)
   const int n_genomes_active = active_genomes(p);
 
   for (;;) {  // genomes, one per workgroup at a time
+    const int t = opaque_tid(), lane = t & 63;
     if (t == 0) ctl[0] = (int)atomicAdd(p.work, 1u);
     __syncthreads();
     const int gi = __builtin_amdgcn_readfirstlane(ctl[0]);  // uniform: the genome loop's exit
@@ -289,7 +331,13 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       g.act_r = g.act_l = g.timeout = g.total = g.frames = 0;
       g.active = 1;
       g.s1b = g.s2b = g.vis = g.lc2 = g.rc2 = g.left = g.pad0 = g.pad1 = 0;
-      games[lane] = g;
+      // (an opaque zero in each of the record's constant 16-B words: constant
+      // words were materialised at kernel entry and kept in scratch till here)
+      const int z = opaque_zero();
+      g.st.bx += z;
+      g.st.vis += z;
+      g.st.point += z;
+      wg_store(&games[lane], g);
       rat[lane] = -1;  // no rally search open
     }
     if (wid == 0) {
@@ -301,12 +349,13 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
     wide_prep<NG, WT>(scratch, lay, gbase + W1n, opponents + W1n, orow, ctl[1], C2, H2, t, w3r, O * C3, W2n);
     PG_STAMP(4);
     for (int fno = 0;; ++fno) {  // frames, all games in lockstep
+      const int t = opaque_tid(), lane = t & 63;
       int *cf = ctl + 8 + (fno & 1) * 32;  // [0] column mask, [1] any active, [2] nets, [3..] net ids
       // ---- A: env.step + find_stuff + inference features (main.py:77-87)
       if (wid == 0) {
         const bool mine = lane < n_games;
         WideGame g;
-        if (mine) g = games[lane];
+        if (mine) g = wg_load(&games[lane]);
         const bool active = mine && g.active;
         if (active && probe) {  // the given doubled centroids (log_wide's k) in place of a frame
           g.vis = 1;
@@ -343,7 +392,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             }
           }
         }
-        if (active) games[lane] = g;
+        if (active) wg_store(&games[lane], g);
         const uint64_t rb = __ballot(active && g.vis);
         const uint64_t lb = __ballot(active && g.vis && g.kind == kOppNN);
         const uint64_t ab = __ballot(active);
@@ -390,8 +439,8 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           Src r;
           r.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
                                                      valid ? (int)lay.net_bytes : 0, 0x00020000);
-          r.soff = tl * 8 * PB;
-          r.toff = (valid && tl == T - 1) ? (uint32_t)(T * 8 * PB + t * 16) : 0x80000000u;
+          r.soff = tl * kPieces * PB;
+          r.toff = (valid && tl == T - 1) ? (uint32_t)(T * kPieces * PB + t * 16) : 0x80000000u;
           return r;
         };
         auto load = [&](const Src &src, int q) -> uint4 {
@@ -406,14 +455,14 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           }
         };
         const bool stream_rows = wid * 64 < H2;  // wave-uniform: a wave past the last row streams nothing
-        uint4 R[kDepth][8], RT[kDepth][kTP];
+        uint4 R[kDepth][kPieces], RT[kDepth][kTP];
         auto prologue = [&]() {
           if (stream_rows) {
 #pragma unroll
             for (int d = 0; d < kDepth; ++d) {
               const Src src = source(d);
 #pragma unroll
-              for (int q = 0; q < 8; ++q) R[d][q] = load(src, q);
+              for (int q = 0; q < kPieces; ++q) R[d][q] = load(src, q);
               load_tail(src, RT[d]);
             }
           }
@@ -508,13 +557,13 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           return (double)tq[i];
         };
         // multiply tile s (in r / rt) into the row sums and load tile sn into r / rt
-        auto compute = [&](int s, uint4 (&r)[8], uint4 (&rt)[kTP], int sn) {
+        auto compute = [&](int s, uint4 (&r)[kPieces], uint4 (&rt)[kTP], int sn) {
           const Src src = source(sn);
           // rows t >= H2 of a partial last wave sum garbage that is never stored
           const bool work = s < S;
           if (!work) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) r[q] = load(src, q);
+            for (int q = 0; q < kPieces; ++q) r[q] = load(src, q);
             load_tail(src, rt);
             return;
           }
@@ -525,7 +574,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           if (net == 0) {
             if (full && wave_k0) {  // the hot case: every element a fused multiply-add
 #pragma unroll
-              for (int q = 0; q < 8; ++q) {
+              for (int q = 0; q < kPieces; ++q) {
                 const uint4 v = r[q];
                 if (!kBurst) r[q] = load(src, q);
                 WT wq[E];
@@ -542,7 +591,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
               }
             } else {
 #pragma unroll
-              for (int q = 0; q < 8; ++q) {
+              for (int q = 0; q < kPieces; ++q) {
                 const uint4 v = r[q];
                 if (!kBurst) r[q] = load(src, q);
                 WT wq[E];
@@ -575,7 +624,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             }
             if (full && wave_k0) {
 #pragma unroll
-              for (int q = 0; q < 8; ++q) {
+              for (int q = 0; q < kPieces; ++q) {
                 const uint4 v = r[q];
                 if (!kBurst) r[q] = load(src, q);
                 WT wq[E];
@@ -589,7 +638,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
               }
             } else {
 #pragma unroll
-              for (int q = 0; q < 8; ++q) {
+              for (int q = 0; q < kPieces; ++q) {
                 const uint4 v = r[q];
                 if (!kBurst) r[q] = load(src, q);
                 WT wq[E];
@@ -609,7 +658,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           }
           if (kBurst) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) r[q] = load(src, q);
+            for (int q = 0; q < kPieces; ++q) r[q] = load(src, q);
           }
           load_tail(src, rt);
         };
@@ -712,7 +761,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
 
       // ---- E: actions, clamp, bookkeeping (main.py:88-107, 128-135)
       if (wid == 0 && lane < n_games) {
-        WideGame g = games[lane];
+        WideGame &g = games[lane];  // in place: the fields phase E touches, read and written in LDS
         if (g.active && probe) {
           p.wide_probe_index[gi] = argmax_np(outv, O);
           if (p.wide_probe_act)
@@ -731,7 +780,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
               left = index_to_code(il);
               if (p.hard_log && near_tie(outv + (NG + lane) * 4, O)) log_wide(p.hard_log, p.counters, p.hard_cap, p.opp[w], 1, il, feat + (NG + lane) * 8);
             }
-            c_fwd += 1 + (g.kind == kOppNN ? 1 : 0);
+            cnt[lane * 4 + 1] += 1 + (g.kind == kOppNN ? 1 : 0);
           }
           g.act_l = clamp_action(g.lc2, left);
           g.act_r = clamp_action(g.rc2, right);
@@ -759,7 +808,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             } else if (rkey[lane] == key) {
               const int rest = kTimeoutThresh + 1 - g.timeout;
               g.frames += rest;
-              c_skip += rest;
+              cnt[lane * 4 + 3] += rest;
               g.timeout = kTimeoutThresh + 1;
             } else if (g.timeout - rat[lane] >= rspan[lane]) {
               rkey[lane] = key;
@@ -771,15 +820,16 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
           if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || g.timeout > kTimeoutThresh) {
             finish_game(p, w, st, g.frames, g.total);
             g.active = 0;
-            c_steps += g.frames;
-            c_games += 1;
+            cnt[lane * 4 + 0] += g.frames;
+            cnt[lane * 4 + 2] += 1;
           }
         }
-        games[lane] = g;
       }
     }
   }
-  if (p.counters && wid == 0 && c_games) {
+  if (p.counters && wid == 0 && lane < NG && cnt[lane * 4 + 2]) {
+    const uint64_t c_steps = cnt[lane * 4], c_fwd = cnt[lane * 4 + 1], c_games = cnt[lane * 4 + 2],
+                   c_skip = cnt[lane * 4 + 3];
     atomicAdd((unsigned long long *)&p.counters[0], (unsigned long long)(c_steps - c_skip));
     if (c_skip) atomicAdd((unsigned long long *)&p.counters[8], (unsigned long long)c_skip);
     atomicAdd((unsigned long long *)&p.counters[1], (unsigned long long)c_fwd);

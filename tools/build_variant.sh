@@ -1,8 +1,8 @@
 #!/bin/bash
 # Build a libpong_ga.so variant with extra defines for one translation unit
-# (default pong_ga.hip: k_service & co.; PG_TU=pg_staged.hip for k_staged),
+# (default pong_ga.hip: k_service & co.; PG_TU=pg_wide.hip for k_wide),
 # linking the main build's other objects: variants/lib_NAME.so.
-# usage: [PG_TU=pg_staged.hip] tools/build_variant.sh NAME [-DFLAG=VALUE ...]   (run the main build first)
+# usage: [PG_TU=pg_wide.hip] tools/build_variant.sh NAME [-DFLAG=VALUE ...]   (run the main build first)
 set -e
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)

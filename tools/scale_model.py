@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Weak-scaling projection of bench.py to N GPUs, measured on one GPU.
+
+BASELINE config 4 (P = N x 65 536 over N GPUs): every rank evaluates its
+shard of 65 536 genomes and repeats the replicated eaSimple work of the whole
+population (select/vary of P rows, the hall-of-fame update) -- DESIGN.md 7.
+This tool measures both terms on one GPU at P = N x 65 536:
+  * per-shard evaluation: after each DeviceGA generation, the shard of every
+    rank is evaluated ON ITS OWN (the same rows, schedule and hall of fame a
+    rank would play; one launch each, HIP events): the slowest shard sets the
+    generation's pace at N (the straggler term), the mean is what N = 1 pays;
+  * replicated work: the generation's wall time minus its evaluation (the
+    fused step's own events) at P = N x 65 536, and the same at 65 536;
+and prints the projected efficiency (N=1 generation time) / (N generation time)
+with t_N = max-shard eval + replicated(P) + all-gather(P) and t_1 = mean-shard
+eval + replicated(65 536).  The all-gather (fitness f64 + lineage f32 per row)
+is priced at 1 TB/s aggregate over xGMI (a conservative reading of 7 x 153
+GB/s links) plus 30 us.
+
+usage: python tools/scale_model.py [N=8] [generations=6]
+"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "neuro-genetic-pong-self-play_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from pong_amd import device as D  # noqa: E402
+from pong_amd.evolve import DeviceGA  # noqa: E402
+
+
+def make_ga(P, dev, seed=1234, sigma=3.0):
+    ga = DeviceGA([6, 64, 3], P, device=dev, schedule="selfplay", seed=seed)
+    ga.initialize("normal", sigma)
+    gen = torch.Generator(device=dev).manual_seed(seed + 1)
+    rows = max(1, (1 << 28) // (8 * ga.G))
+    for r0 in range(0, ga.H, rows):
+        r1 = min(ga.H, r0 + rows)
+        ga.store[r0:r1] = torch.randn((r1 - r0, ga.G), generator=gen, dtype=torch.float64, device=dev).mul_(sigma)
+    ga.set_hall_of_fame(None, np.full(ga.H, -1e300))
+    return ga
+
+
+def timed_steps(ga, steps):
+    """(wall ms, evaluation ms) per generation, steady state."""
+    out = []
+    for _ in range(steps):
+        ga.eval_events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ga.step()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
+        out.append((wall, ga.eval_events[0].elapsed_time(ga.eval_events[1])))
+    ga.eval_events = None
+    return out
+
+
+def shard_evals(ga, n_shards):
+    """Each rank's shard of the current population evaluated on its own (ms each)."""
+    P, S = ga.P, ga.P // n_shards
+    ev = D.Evaluator(ga.nodes, dtype=ga.dtype, device=ga.device, n_games=ga.n_games, seed=ga.ev.seed)
+    opponents = ga.hall_of_fame[: ga.hof_n]
+    ms = []
+    for r in range(n_shards):
+        lo = r * S
+        kind, opp, mult = D.schedule("selfplay", S, ga.n_games, lo, ga.hof_fitness, ga.hof_n, ga.seed,
+                                     ga.generation + 1, ga.device)
+        rows = ga.population[lo:lo + S]
+        ev.evaluate(rows, kind, opp, mult, opponents=opponents, validate=False)  # warm (workspace)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ev.evaluate(rows, kind, opp, mult, opponents=opponents, validate=False)
+        b.record()
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+    return ms
+
+
+def replicated_ops(ga, reps=3):
+    """Device ms of the work every rank repeats for the whole population, one
+    op at a time on the GA's current state (HIP events, median of reps):
+    merge of P fitness values, the hall-of-fame candidates' prepare (hashes,
+    ranks), selTournament by rank sampling, varAnd of P offspring rows, the
+    clones' inherited fitness, the new members' commit; and the host scan."""
+    P, dev = ga.P, ga.device
+    out = {}
+
+    def timed(name, fn):
+        ms = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            r = fn()
+            b.record()
+            torch.cuda.synchronize()
+            ms.append(a.elapsed_time(b))
+        out[name] = float(np.median(ms))
+        return r
+
+    fit = ga.fitness.clone()
+    worst = float(ga._hof_fit_host[-1]) if ga.hof_n >= ga.H else None
+    new_fit = torch.empty_like(fit)
+    cand = torch.empty(P, dtype=torch.int32, device=dev)
+    cand_fit = torch.empty(P, dtype=torch.float64, device=dev)
+    summ = torch.empty(8, dtype=torch.float64, device=dev)
+    # fitness perturbed so that a steady-state share of rows beats the worst member
+    timed("merge", lambda: D.merge_fitness(fit, None, None, new_fit, worst, cand, cand_fit, summ, ga.ws))
+    k = int(summ[6].item())
+    out["candidates"] = k
+    chosen = torch.empty(P, dtype=torch.int32, device=dev)
+    timed("select_ranked", lambda: D.select_ranked(fit, P, ga.tournsize, ga.seed, 99, ga.ws, chosen=chosen))
+    offspring = ga.spare[ga.H:]
+    timed("vary", lambda: D.vary(ga.population, chosen, ga.G, ga.cxpb, ga.mutpb, ga.alpha, ga.mu, ga.sigma,
+                                 ga.indpb, seed=ga.seed, generation=99, out=offspring))
+    inherited = torch.empty(P, dtype=torch.float64, device=dev)
+    lin = torch.empty(P, dtype=torch.float32, device=dev)
+    timed("inherit", lambda: D.inherit(chosen, fit, inherited, ga.lineage_frames, lin))
+    if k:
+        old_n = ga.hof_n
+        ch = torch.empty(k, dtype=torch.int64, device=dev)
+        pk = torch.empty(old_n + 2 * k, dtype=torch.int64, device=dev)
+        timed("hof_prepare", lambda: D.hof_prepare_cand(ga.hof_fitness[:old_n], ga.hof_hash[:old_n], cand[:k],
+                                                       cand_fit[:k], ga.population, ga.G, ch, pk, ga.ws))
+        pk_h = pk.cpu().numpy()
+        n = old_n + k
+        t0 = time.perf_counter()
+        src, nf = D.hof_update(ga.H, ga._hof_fit_host, (pk_h[:old_n] >> 32), pk_h[n:].view(np.float64),
+                               pk_h[old_n:n] >> 32, rank=(pk_h[:n] & 0xFFFFFFFF).astype(np.int32))
+        out["hof_scan_host"] = (time.perf_counter() - t0) * 1e3
+        m = src.shape[0]
+        src_d = torch.tensor(src, dtype=torch.int32, device=dev)
+        nf_d = torch.tensor(nf, dtype=torch.float64, device=dev)
+        hh = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
+        hf = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
+        dst = torch.empty((m, ga.G), dtype=ga.dtype, device=dev)
+        timed("hof_commit", lambda: D.hof_commit(dst, ga.store, ga.population, cand[:k], src_d, old_n, ga.G,
+                                                 ga.hof_hash, ch, hh, nf_d, hf))
+    dev_serial = out.get("merge", 0) + out.get("hof_prepare", 0) + out.get("hof_commit", 0)
+    overlapped = max(out["select_ranked"] + out["vary"] + out["inherit"], out.get("hof_scan_host", 0.0))
+    out["replicated_critical_ms"] = dev_serial + overlapped
+    return out
+
+
+def main():
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    gens = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    dev = torch.device("cuda", 0)
+    S = 65536
+    res = {"N": N, "shard": S}
+    # replicated work at one GPU's population
+    ga1 = make_ga(S, dev)
+    for _ in range(3):
+        ga1.step()
+    t1 = timed_steps(ga1, gens)
+    res["p65536_wall_ms"] = [w for w, _ in t1]
+    res["p65536_eval_ms"] = [e for _, e in t1]
+    del ga1
+    torch.cuda.empty_cache()
+    # the N-GPU population on one GPU
+    gaN = make_ga(N * S, dev)
+    for _ in range(3):
+        gaN.step()
+    walls, evals, shards = [], [], []
+    for g in range(gens):
+        (w, e), = timed_steps(gaN, 1)
+        walls.append(w)
+        evals.append(e)
+        sh = shard_evals(gaN, N)
+        shards.append(sh)
+        print(json.dumps({"gen": gaN.generation, "wall_ms": w, "eval_ms": e, "shard_ms": sh}), flush=True)
+    ops = replicated_ops(gaN)
+    print(json.dumps({"replicated_ops_pN": ops}), flush=True)
+    res["replicated_ops_pN"] = ops
+    repl1 = float(np.median([w - e for w, e in t1]))
+    # a rank at N repeats the population-wide ops of P = N x 65 536 where the
+    # one-GPU run pays them for 65 536, and its shard-sized work (evaluation
+    # prep, order, scatter) as at N = 1
+    replN = repl1 + ops["replicated_critical_ms"] * (1.0 - 1.0 / N)
+    res["replicated_ms_pN_wall"] = float(np.median([w - e for w, e in zip(walls, evals)]))
+    shard_max = float(np.median([max(s) for s in shards]))
+    shard_mean = float(np.median([float(np.mean(s)) for s in shards]))
+    allgather = 0.03 + N * S * 12 / 1e12 * 1e3  # ms
+    t_n = shard_max + replN + allgather
+    t_1 = shard_mean + repl1
+    res.update({"replicated_ms_p65536": repl1, "replicated_ms_pN": replN, "shard_eval_ms_max": shard_max,
+                "shard_eval_ms_mean": shard_mean, "straggler_factor": shard_max / shard_mean,
+                "allgather_ms_model": allgather, "t1_ms": t_1, "tN_ms": t_n, "projected_efficiency": t_1 / t_n,
+                "projected_speedup": N * t_1 / t_n})
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
