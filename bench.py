@@ -470,7 +470,20 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
             "c_port": {"value": steps / dt if dt > 0 else None, "cores": workers,
                        "sample": f"C restatement (oracle/pong_oracle.c, OpenMP over {workers} threads): "
                                  f"{done} genomes x {args.games} games ({steps} env-steps in {dt:.1f} s)"},
-            "cpu": _cpu_model()}
+            "cpu": _cpu_model(),
+            "host_cpus": _host_cpus(workers),
+            "full_box": _full_box(rate_p, workers)}
+
+
+def _full_box(rate_p, workers):
+    """SURVEY 8(d)'s whole-node CPU figure: os.cpu_count() cores at the pooled
+    per-core rate.  Extrapolated, not run -- the job's cgroup grants 16 CPUs of
+    time (``host_cpus``), and a pool of os.cpu_count() processes would
+    time-slice those same 16."""
+    n = os.cpu_count() or workers
+    per_core = rate_p / workers if workers else None
+    return {"cores": n, "value": per_core * n if per_core else None, "per_core": per_core,
+            "kind": "extrapolated: pooled per-core rate x os.cpu_count()"}
 
 
 def _pmc(name):
@@ -507,6 +520,30 @@ def _pmc_stale(pmc):
 def _pmc_traffic(name="pmc_traffic.json"):
     pmc, _ = _pmc(name)
     return pmc.get("traffic_bytes") if pmc else None
+
+
+def _host_cpus(workers):
+    """What the box lets this job use (SURVEY 8(d) asks for a pool of
+    os.cpu_count() processes): the visible CPUs, this process's affinity, and
+    the cgroup's CPU quota -- on the MI355X boxes os.cpu_count() shows the whole
+    node (256) while cpu.max grants 16 CPUs of time, so a 16-process pool is the
+    full box available to the job and a larger pool would only time-slice it."""
+    out = {"os_cpu_count": os.cpu_count(), "pool_processes": workers}
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        out["cgroup_cpu_max"] = f"{q} {per}"
+        if q != "max":
+            out["cgroup_cpus"] = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    quota = out.get("cgroup_cpus")
+    out["pool_is_full_quota"] = bool(quota is not None and workers >= quota)
+    return out
 
 
 def _cpu_model():

@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 8
+#define PG_ABI_VERSION 9
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -278,6 +278,14 @@ typedef struct pg_ga_args {
   double mu, sigma, indpb;       /* GAUSSIAN_MUTATION_MEAN/SIGMA, PROBABILITY_OF_MUTATING_A_SINGLE_GENE */
   uint64_t seed;                 /* RNG key: (seed, generation) */
   uint64_t generation;
+  /* ABI 9: [(n + 1) / 2] or NULL.  Non-NULL: only the pairs (2j, 2j + 1) with
+   * pair_mask[j] != 0 are written to offspring (invalid[] is written for every
+   * row either way).  Every offspring row is a pure function of its pair's
+   * parent rows and the (seed, generation) keys, so rows varied in separate
+   * calls equal one full call's: a rank of a sharded run varies its shard
+   * first and, once the fitness all-gather has named them, the hall-of-fame
+   * candidates and the next selection's parents. */
+  const uint8_t *pair_mask;
 } pg_ga_args;
 
 typedef struct pg_select_args {
@@ -417,6 +425,11 @@ int32_t pg_ga_select_tournament(const pg_select_args *args, void *stream);
 int32_t pg_ga_select_tournament_ranked(const pg_select_args *args, const double *sorted_fitness,
                                        const int32_t *order, void *stream);
 int32_t pg_ga_vary(const pg_ga_args *args, void *stream);
+/* pair_mask[rows[i] >> 1] = 1 for i < n_rows, except pairs in [skip_lo, skip_hi)
+ * and pairs j with exclude[j] != 0 (exclude [n_pairs] or NULL; mask [n_pairs];
+ * rows outside [0, 2 n_pairs) are skipped). */
+int32_t pg_ga_mark_pairs(uint8_t *pair_mask, int32_t n_pairs, const int32_t *rows, int32_t n_rows,
+                         int32_t skip_lo, int32_t skip_hi, const uint8_t *exclude, void *stream);
 int32_t pg_ga_schedule(const pg_schedule_args *args, void *stream);
 /* hash[i] = 64-bit hash of the genes of row index[i] (row i if index is NULL):
  * f32/f64 bit patterns, -0.0 as 0.0, so equal gene lists hash equal. */

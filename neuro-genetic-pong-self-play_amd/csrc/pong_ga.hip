@@ -479,9 +479,14 @@ __global__ __launch_bounds__(256) void k_vary(pg_ga_args a) {
   const int i0 = 2 * pair, i1 = 2 * pair + 1;
   const bool has1 = i1 < a.n;
   const bool cx = has1 && rng_u01(rng_key(a.seed, a.generation, 2, (uint64_t)pair), 0) < a.cxpb;
-  const uint64_t k3 = rng_key(a.seed, a.generation, 3, (uint64_t)pair);
   const bool mut0 = rng_u01(rng_key(a.seed, a.generation, 4, (uint64_t)i0), 0) < a.mutpb;
   const bool mut1 = has1 && rng_u01(rng_key(a.seed, a.generation, 4, (uint64_t)i1), 0) < a.mutpb;
+  if (lane == 0) {
+    a.invalid[i0] = (uint8_t)(cx || mut0);
+    if (has1) a.invalid[i1] = (uint8_t)(cx || mut1);
+  }
+  if (a.pair_mask && !a.pair_mask[pair]) return;  // a pair this call does not write (pong_ga.h)
+  const uint64_t k3 = rng_key(a.seed, a.generation, 3, (uint64_t)pair);
   const uint64_t k5 = rng_key(a.seed, a.generation, 5, (uint64_t)pair);
   const uint64_t k6 = rng_key(a.seed, a.generation, 6, (uint64_t)pair);
   const WT *p1 = (const WT *)a.parents + (long)a.chosen[i0] * a.stride;
@@ -539,10 +544,16 @@ __global__ __launch_bounds__(256) void k_vary(pg_ga_args a) {
       }
     }
   }
-  if (lane == 0) {
-    a.invalid[i0] = (uint8_t)(cx || mut0);
-    if (has1) a.invalid[i1] = (uint8_t)(cx || mut1);
-  }
+}
+
+__global__ void k_mark_pairs(uint8_t *mask, int n_pairs, const int32_t *rows, int n_rows, int skip_lo, int skip_hi,
+                             const uint8_t *exclude) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rows) return;
+  const int r = rows[i];
+  if (r < 0 || r >= 2 * n_pairs) return;
+  const int j = r >> 1;
+  if ((j < skip_lo || j >= skip_hi) && !(exclude && exclude[j])) mask[j] = 1;
 }
 
 // Opponent schedule of evaluate() (main.py:28-66) for rows [0, n).
@@ -1121,6 +1132,17 @@ int32_t pg_ga_vary(const pg_ga_args *a, void *stream) {
     hipLaunchKernelGGL(k_vary<double>, grid, dim3(256), 0, (hipStream_t)stream, *a);
   else
     hipLaunchKernelGGL(k_vary<float>, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_ga_mark_pairs(uint8_t *mask, int32_t n_pairs, const int32_t *rows, int32_t n_rows, int32_t skip_lo,
+                         int32_t skip_hi, const uint8_t *exclude, void *stream) {
+  if (n_pairs < 0 || n_rows < 0 || (n_rows && (!mask || !rows)))
+    return fail(PG_ERR_INVALID, "mark_pairs: bad sizes or NULL buffers");
+  if (n_rows == 0) return PG_OK;
+  hipLaunchKernelGGL(k_mark_pairs, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mask,
+                     n_pairs, rows, n_rows, skip_lo, skip_hi, exclude);
   PG_HIP(hipGetLastError());
   return PG_OK;
 }

@@ -16,7 +16,7 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 8
+PG_ABI_VERSION = 9
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -89,7 +89,7 @@ class PgGaArgs(ctypes.Structure):
         ("chosen", _vp), ("offspring", _vp), ("invalid", _vp),
         ("cxpb", ctypes.c_double), ("mutpb", ctypes.c_double), ("alpha", ctypes.c_double),
         ("mu", ctypes.c_double), ("sigma", ctypes.c_double), ("indpb", ctypes.c_double),
-        ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64),
+        ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64), ("pair_mask", _vp),
     ]
 
 
@@ -187,6 +187,8 @@ SIGNATURES = {
     "pg_ga_select_tournament": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp]),
     "pg_ga_select_tournament_ranked": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp, _vp, _vp]),
     "pg_ga_vary": (ctypes.c_int32, [ctypes.POINTER(PgGaArgs), _vp]),
+    "pg_ga_mark_pairs": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                          _vp, _vp]),
     "pg_ga_schedule": (ctypes.c_int32, [ctypes.POINTER(PgScheduleArgs), _vp]),
     "pg_row_hash": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp,
                                      _vp]),

@@ -95,8 +95,10 @@ def _config(ga) -> dict:
 
 
 def save(ga, path: str) -> str:
-    """Write the DeviceGA state (population, fitness, hall of fame, generation, logbook)."""
-    tensors = {"population": ga.population, "fitness": ga.fitness, "valid": ga.valid.to(torch.uint8),
+    """Write the DeviceGA state (population, fitness, hall of fame, generation,
+    logbook).  A sharded run (ga.shard_vary) holds only its shard's rows of
+    the population: every rank calls save (one all-gather of the rows)."""
+    tensors = {"population": ga.population_full(), "fitness": ga.fitness, "valid": ga.valid.to(torch.uint8),
                "hall_of_fame": ga.hall_of_fame,
                "hof_fitness": torch.from_numpy(np.ascontiguousarray(ga.hof_member_fitness))}
     meta = {"format": FORMAT, "config": json.dumps(_config(ga)), "generation": ga.generation,

@@ -370,25 +370,47 @@ def select_tournament_ranked(fitness: torch.Tensor, k: int, tournsize: int, seed
 
 
 def vary(parents: torch.Tensor, chosen: torch.Tensor, genes: int, cxpb: float, mutpb: float, alpha: float,
-         mu: float, sigma: float, indpb: float, seed: int, generation: int, out: Optional[torch.Tensor] = None):
-    """algorithms.varAnd(cxBlend, mutGaussian) on device: returns (offspring, invalid[n] uint8)."""
+         mu: float, sigma: float, indpb: float, seed: int, generation: int, out: Optional[torch.Tensor] = None,
+         pair_mask: Optional[torch.Tensor] = None, invalid: Optional[torch.Tensor] = None):
+    """algorithms.varAnd(cxBlend, mutGaussian) on device: returns (offspring, invalid[n] uint8).
+    ``pair_mask`` ([(n + 1) // 2] uint8): only the marked pairs' rows are
+    written (the invalid flags of every row are); see pg_ga_args.pair_mask."""
     dev = parents.device
     n = chosen.shape[0]
     _need(chosen, "chosen", torch.int32, dev, (n,))
+    if pair_mask is not None:
+        _need(pair_mask, "pair_mask", torch.uint8, dev, ((n + 1) // 2,))
     if out is None:
         out = torch.empty((n, parents.shape[1]), dtype=parents.dtype, device=dev)
-    invalid = torch.empty(n, dtype=torch.uint8, device=dev)
+    if invalid is None:
+        invalid = torch.empty(n, dtype=torch.uint8, device=dev)
+    _need(invalid, "invalid", torch.uint8, dev, (n,))
     a = L.PgGaArgs()
     a.n, a.genes, a.dtype = n, genes, DTYPES[parents.dtype]
     a.parents, a.stride, a.n_parents = _ptr(parents), parents.stride(0), parents.shape[0]
     a.chosen, a.offspring, a.invalid = _ptr(chosen), _ptr(out), _ptr(invalid)
     a.cxpb, a.mutpb, a.alpha, a.mu, a.sigma, a.indpb = cxpb, mutpb, alpha, mu, sigma, indpb
     a.seed, a.generation = seed, generation
+    a.pair_mask = _ptr(pair_mask)
     if out.stride(0) != parents.stride(0):
         raise ValueError("offspring and parents must share the row stride")
     with torch.cuda.device(dev):
         L.check("pg_ga_vary", L.lib().pg_ga_vary(ctypes.byref(a), _stream(dev)))
     return out, invalid
+
+
+def mark_pairs(mask: torch.Tensor, rows: torch.Tensor, skip: tuple = (0, 0),
+               exclude: Optional[torch.Tensor] = None) -> None:
+    """pg_ga_mark_pairs: mask[rows >> 1] = 1 except the pairs in [skip[0],
+    skip[1]) and those ``exclude`` marks."""
+    dev = mask.device
+    _need(mask, "pair_mask", torch.uint8, dev)
+    _need(rows, "rows", torch.int32, dev)
+    if exclude is not None:
+        _need(exclude, "exclude", torch.uint8, dev, tuple(mask.shape))
+    with torch.cuda.device(dev):
+        L.check("pg_ga_mark_pairs", L.lib().pg_ga_mark_pairs(_ptr(mask), mask.shape[0], _ptr(rows), rows.numel(),
+                                                             int(skip[0]), int(skip[1]), _ptr(exclude), _stream(dev)))
 
 
 SCHEDULES = {"reference": L.PG_SCHED_REFERENCE, "selfplay": L.PG_SCHED_SELFPLAY}

@@ -51,6 +51,12 @@ def gather_fitness(local: torch.Tensor, n_total: int, group=None) -> torch.Tenso
     return torch.cat(parts).to(local.device)
 
 
+def gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
+    """All-gather each rank's shard rows ([rows, ...]) into the full table in
+    row order (gather_fitness for any row width: genomes, hashes)."""
+    return gather_fitness(local, n_total, group)
+
+
 def evaluate_sharded(evaluate_rows, n_total: int, group=None):
     """Evaluate this rank's rows with ``evaluate_rows(lo, hi) -> fitness tensor``
     and return the full fitness vector on every rank."""

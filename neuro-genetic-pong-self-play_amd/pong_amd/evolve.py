@@ -19,6 +19,17 @@ variation nor the hall-of-fame gather reads what it writes.  The GA state is
 replicated on every rank; rank r evaluates rows ``shard_range(P, r, N)`` and
 the fitness vector is all-gathered once per generation -- the only collective.
 
+Sharded variation (``shard_vary``, on when N > 1): a rank writes only the
+offspring rows it needs -- its shard's before the evaluation, then, once the
+all-gathered fitness names them, the hall-of-fame candidates and the parents
+the next selection picks (tournaments of P/4 draws pick the top rows and their
+tied clones: 5 242 distinct of 524 288 in tools/scale_model.py, nearly all of
+them candidates too).  Every offspring row is a pure function of its pair's parent
+rows and the (seed, generation) keys (pg_ga_args.pair_mask), so these rows
+equal a full varAnd's and the replicated state stays identical across ranks;
+the other rows of ``population`` are not current on this rank
+(``population_full()`` all-gathers the shards).
+
 Differences from DEAP (DESIGN.md "GA"): random draws are counter-based
 (distribution parity, not Mersenne-Twister stream parity); ``similar`` is the
 equality of 64-bit gene hashes; only the invalid offspring are evaluated
@@ -104,6 +115,16 @@ class DeviceGA:
         # launches and two host syncs (csrc/pg_gen.hip): False runs the torch
         # formulation above (the cross-check of tests/test_gpu_generation.py)
         self.fused = True
+        # the fused path runs the next generation's select/vary beside the
+        # hall-of-fame update on a second HIP stream (False: one stream, the A/B)
+        self.side_stream = True
+        self._side = None
+        # sharded variation (module docstring; fused path): at N = 1 the shard is
+        # the whole population and there is nothing to leave out
+        self.shard_vary = self.world > 1
+        self._n_pairs = (self.P + 1) // 2
+        self._skip = (self.lo >> 1, (self.hi + 1) >> 1) if self.hi > self.lo else (0, 0)
+        self._shard_pairs = None
         self.ws = D.Workspaces(self.device)
         self._lineage_alt = torch.zeros_like(self.lineage_frames)
         self._hof_hash_alt = torch.zeros_like(self.hof_hash)
@@ -115,6 +136,24 @@ class DeviceGA:
     @property
     def population(self) -> torch.Tensor:
         return self.store[self.H:]
+
+    def population_full(self) -> torch.Tensor:
+        """The whole current population on this rank: ``population`` itself, or
+        with sharded variation the ranks' shard rows all-gathered (a
+        collective: every rank calls it)."""
+        if not self._sharded():
+            return self.population
+        return PD.gather_rows(self.population[self.lo:self.hi].contiguous(), self.P, self.group)
+
+    def population_hash(self) -> torch.Tensor:
+        """pg_row_hash of every population row ([P] int64; sharded: each rank
+        hashes its shard and the 8-B hashes are all-gathered)."""
+        if not self._sharded():
+            return D.row_hash(self.population, self.G)
+        return PD.gather_rows(D.row_hash(self.population[self.lo:self.hi], self.G), self.P, self.group)
+
+    def _sharded(self) -> bool:
+        return bool(self.shard_vary and self.fused and self.world > 1 and dist.is_initialized())
 
     @property
     def hall_of_fame(self) -> torch.Tensor:
@@ -406,13 +445,50 @@ class DeviceGA:
     def _buf(self, name, shape, dtype):
         return self.ws.tensor(name, shape, dtype)
 
-    def _next_gen_prep(self, g: int, parents: torch.Tensor, fitness: torch.Tensor, store: torch.Tensor):
-        """Generation g's selTournament + varAnd into store[H:], what the clones
-        inherit, and the shard's evaluation order; kept in self._next."""
-        chosen = self._buf("chosen", self.P, torch.int32)
+    def _select(self, g: int, fitness: torch.Tensor) -> torch.Tensor:
+        """Generation g's selTournament (rows of generation g - 1), in the
+        buffer of g's parity: generation g - 1's stays readable meanwhile."""
+        chosen = self._buf("chosen%d" % (g & 1), self.P, torch.int32)
         D.select_ranked(fitness, self.P, self.tournsize, self.seed, g, self.ws, chosen=chosen)
+        return chosen
+
+    def _shard_mask(self) -> torch.Tensor:
+        """The pairs of this rank's shard rows (fixed for the run)."""
+        if self._shard_pairs is None:
+            self._shard_pairs = torch.zeros(self._n_pairs, dtype=torch.uint8, device=self.device)
+            self._shard_pairs[self._skip[0]:self._skip[1]] = 1
+        return self._shard_pairs
+
+    def _complete(self, g: int, off: torch.Tensor, parents: torch.Tensor, rows: torch.Tensor, name: str,
+                  exclude: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Sharded variation: generation g's rows ``rows`` of ``off`` beyond this
+        rank's shard (and beyond the pairs ``exclude`` marks), varied from
+        generation g - 1's rows ``parents`` (their parents: rows an earlier
+        completion made current) with generation g's selection; returns the
+        pair mask written."""
+        mask = self._buf("complete_" + name, self._n_pairs, torch.uint8)
+        mask.zero_()
+        D.mark_pairs(mask, rows, skip=self._skip, exclude=exclude)
+        chosen = self._buf("chosen%d" % (g & 1), self.P, torch.int32)
+        D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu, self.sigma, self.indpb,
+               seed=self.seed, generation=g, out=off, pair_mask=mask,
+               invalid=self._buf("complete_inv_" + name, self.P, torch.uint8))
+        return mask
+
+    def _next_gen_prep(self, g: int, parents: torch.Tensor, fitness: torch.Tensor, store: torch.Tensor,
+                       cand_pairs: Optional[torch.Tensor] = None):
+        """Generation g's selTournament + varAnd into store[H:] (sharded: this
+        rank's shard rows), what the clones inherit, and the shard's
+        evaluation order; kept in self._next.  Sharded, after generation
+        g - 1's evaluation (``cand_pairs``: the pairs its candidates' completion
+        wrote): first generation g - 1's rows that this selection picked as
+        parents, from store[H:] (generation g - 2) before it is overwritten."""
+        chosen = self._select(g, fitness)
+        if cand_pairs is not None:
+            self._complete(g - 1, parents, store[self.H:], chosen, "parents", exclude=cand_pairs)
         _, inv = D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu, self.sigma, self.indpb,
-                        seed=self.seed, generation=g, out=store[self.H:])
+                        seed=self.seed, generation=g, out=store[self.H:],
+                        pair_mask=self._shard_mask() if self._sharded() else None)
         inherited = self._buf("inherited", self.P, torch.float64)
         D.inherit(chosen, fitness, inherited, self.lineage_frames, self._lineage_alt)
         self.lineage_frames, self._lineage_alt = self._lineage_alt, self.lineage_frames
@@ -515,6 +591,22 @@ class DeviceGA:
             return
         if self.profile is not None:
             self.profile["hof_candidates"] = self.profile.get("hof_candidates", 0) + k
+        # the next generation's select/vary/inherit/order/early prep depend only
+        # on this generation's fitness: on a side stream from here, beside the
+        # candidates' prepare, the host scan and the commit (the buffers are
+        # disjoint: they write store[H:], the update reads rows and store[:old_n]
+        # and writes dst[:m]); the next evaluation waits for both streams
+        main = torch.cuda.current_stream(self.device)
+        side = None
+        if overlap and self.side_stream:
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            side = self._side
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                overlap()
+            overlap = None
+            self._keep_on(main)
         n = old_n + k
         cand, cand_fit = cand[:k], cand_fit[:k]
         cand_hash = self._buf("cand_hash", k, torch.int64)
@@ -548,6 +640,19 @@ class DeviceGA:
         self.hof_fitness, self._hof_fitness_alt = self._hof_fitness_alt, self.hof_fitness
         self.hof_n = int(m)
         self._hof_fit_host = new_fit
+        if side is not None:
+            main.wait_stream(side)
+
+    def _keep_on(self, stream):
+        """The side stream's fresh tensors in self._next are read on ``stream``
+        later: tell the caching allocator (record_stream) so their memory is not
+        handed out again before that work is done."""
+        if self._next is None:
+            return
+        for t in self._next[1:]:
+            for x in (t if isinstance(t, tuple) else (t,)):
+                if isinstance(x, torch.Tensor) and x.is_cuda:
+                    x.record_stream(stream)
 
     def _step_fused(self) -> dict:
         worst = float(self._hof_fit_host[-1]) if (self.H and self.hof_n >= self.H) else None
@@ -556,7 +661,8 @@ class DeviceGA:
             fit = self._evaluate_fused(0, self.population, self._order(inv))
             new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, self.fitness, worst)
             self.fitness, self.valid = new_fit, torch.ones_like(self.valid)
-            # generation 1's offspring go to spare[H:] (no swap after the initial update)
+            # generation 1's offspring go to spare[H:] (no swap after the initial
+            # update); the initial population is current on every rank
             self._hof_update_fused(self.population, cand, cand_fit, k, self.spare,
                                    overlap=lambda: self._next_gen_prep(1, self.population, new_fit, self.spare))
             self.store[: self.hof_n] = self.spare[: self.hof_n]
@@ -573,11 +679,19 @@ class DeviceGA:
         fit = self._evaluate_fused(g, off, order, sched)  # invalid_ind only: clones keep their parent's fitness
         new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, inherited, worst)
         self._mark("evaluate")
+        cand_pairs = None
+        if self._sharded():
+            # the candidates' rows of this offspring beyond the shard (the update
+            # hashes and gathers them); the next selection's parents follow on
+            # the side stream (_next_gen_prep), both before generation g + 1's
+            # variation overwrites store[H:]
+            cand_pairs = self._complete(g, off, self.population, cand[:k], "cand")
+            self._mark("complete", sub=True)
         # generation g + 1's parents are this offspring; its offspring go to
         # store[H:] (this generation's parents, free now), the buffer the swap
         # below makes next step's spare[H:]
         self._hof_update_fused(off, cand, cand_fit, k, self.spare,
-                               overlap=lambda: self._next_gen_prep(g + 1, off, new_fit, self.store))
+                               overlap=lambda: self._next_gen_prep(g + 1, off, new_fit, self.store, cand_pairs))
         self._mark("hall_of_fame")
         self.fitness = new_fit
         self.store, self.spare = self.spare, self.store

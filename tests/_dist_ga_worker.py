@@ -5,6 +5,7 @@ saves the final state.
 usage: python _dist_ga_worker.py OUT_DIR            (small: [6,8,3], P 101, 3 generations)
        python _dist_ga_worker.py OUT_DIR config4    (BASELINE config 4: [6,64,3], P 524 288,
                                                      self-play vs P/4 hall of fame, 2 generations)
+At world > 1 DeviceGA varies only each rank's shard (shard_vary).
 """
 import json
 import os
@@ -59,9 +60,10 @@ def main(out_dir, mode="small"):
         step_ms = (time.perf_counter() - t0) * 1e3
         phases = dict(ga.profile)
         ga.profile = None
+        # sharded variation: each rank holds its shard's rows; the hashes are all-gathered
+        h = ga.population_hash().cpu().numpy()
         if not dist.is_initialized() or dist.get_rank() == 0:
             os.makedirs(out_dir, exist_ok=True)
-            h = D.row_hash(ga.population, ga.G).cpu().numpy()
             np.save(os.path.join(out_dir, "pop_hash.npy"), h)
             np.save(os.path.join(out_dir, "fitness.npy"), ga.fitness.cpu().numpy())
             np.save(os.path.join(out_dir, "hof_hash.npy"), D.row_hash(ga.hall_of_fame, ga.G).cpu().numpy())
@@ -74,9 +76,10 @@ def main(out_dir, mode="small"):
         ga = DeviceGA([6, 8, 3], 101, hof_size=20, tournsize=9, device=dev, schedule="reference", seed=77)
         ga.initialize("normal", 2.0)
         ga.run(3)
+        pop = ga.population_full().cpu().numpy()  # (sharded variation: an all-gather of the shards' rows)
         if not dist.is_initialized() or dist.get_rank() == 0:
             os.makedirs(out_dir, exist_ok=True)
-            np.save(os.path.join(out_dir, "population.npy"), ga.population.cpu().numpy())
+            np.save(os.path.join(out_dir, "population.npy"), pop)
             np.save(os.path.join(out_dir, "fitness.npy"), ga.fitness.cpu().numpy())
             np.save(os.path.join(out_dir, "hof.npy"), ga.hall_of_fame.cpu().numpy())
             np.save(os.path.join(out_dir, "hof_fitness.npy"), ga.hof_member_fitness)

@@ -176,3 +176,45 @@ def test_hof_prepare_cand_same_scan_as_rank_classes(gpu, hn, k, dup):
         else:
             np.testing.assert_array_equal(first[0], got[0])
             np.testing.assert_array_equal(first[1], got[1])
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_vary_pair_mask_equals_full_vary(gpu, dtype):
+    """pg_ga_args.pair_mask (sharded variation): a shard's pairs, then
+    the pairs pg_ga_mark_pairs marks for scattered rows (outside the shard),
+    written in two calls into one buffer, equal a full varAnd on those rows;
+    unmarked rows are left as they were; the invalid flags are every row's."""
+    from pong_amd import device as D
+    P, G = 1001, 67
+    g = torch.Generator(device=gpu).manual_seed(5)
+    parents = torch.randn((P, G), generator=g, dtype=torch.float64, device=gpu).to(dtype)
+    chosen = torch.randint(0, P, (P,), generator=g, device=gpu, dtype=torch.int32)
+    kw = dict(cxpb=0.9, mutpb=0.9, alpha=0.9, mu=0.0, sigma=0.9, indpb=0.9, seed=3, generation=7)
+    full, inv_full = D.vary(parents, chosen, G, **kw)
+    pairs = (P + 1) // 2
+    lo, hi = 333, 667  # the shard's rows: pairs [166, 334)
+    skip = (lo >> 1, (hi + 1) >> 1)
+    shard = torch.zeros(pairs, dtype=torch.uint8, device=gpu)
+    shard[skip[0]:skip[1]] = 1
+    out = torch.full((P, G), 7.0, dtype=dtype, device=gpu)
+    _, inv = D.vary(parents, chosen, G, **kw, out=out, pair_mask=shard)
+    assert torch.equal(inv, inv_full)
+    rows = torch.tensor([0, 5, 400, 998, 1000, 5, -3, 1001, 2 * pairs + 7], dtype=torch.int32, device=gpu)
+    more = torch.zeros(pairs, dtype=torch.uint8, device=gpu)
+    D.mark_pairs(more, rows, skip=skip)
+    excl = torch.zeros(pairs, dtype=torch.uint8, device=gpu)
+    excl[499] = 1
+    none = torch.zeros(pairs, dtype=torch.uint8, device=gpu)
+    D.mark_pairs(none, rows, skip=skip, exclude=excl)
+    assert none.nonzero().flatten().tolist() == [0, 2, 500]
+    want = torch.zeros(pairs, dtype=torch.uint8)
+    want[[0, 2, 499, 500]] = 1  # row 400's pair (200) is in the shard; -3, 1001 (pair 500 is row 1000's) ...
+    assert more.cpu().tolist() == want.tolist()
+    _, inv2 = D.vary(parents, chosen, G, **kw, out=out, pair_mask=more)
+    assert torch.equal(inv2, inv_full)
+    written = torch.zeros(P, dtype=torch.bool)
+    for j in list(range(skip[0], skip[1])) + [0, 2, 499, 500]:
+        written[2 * j: min(2 * j + 2, P)] = True
+    w = written.to(gpu)
+    assert torch.equal(out[w], full[w])
+    assert bool((out[~w] == 7.0).all())

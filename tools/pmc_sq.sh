@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters of the evaluation kernel for one variant.
-# usage: tools/pmc_resident.sh TAG LANES [LIB]
+# usage: tools/pmc_sq.sh TAG LANES [LIB]
 TAG=$1; LANES=$2; LIB=$3
 OUT=gpurun_out/$TAG; mkdir -p $OUT; ROOT=$(pwd); export TMPDIR=/tmp
 [ -n "$LIB" ] && export PONG_GA_LIB=$ROOT/$LIB

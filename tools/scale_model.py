@@ -4,13 +4,17 @@
 BASELINE config 4 (P = N x 65 536 over N GPUs): every rank evaluates its
 shard of 65 536 genomes and repeats the replicated eaSimple work of the whole
 population (select/vary of P rows, the hall-of-fame update) -- DESIGN.md 7.
-This tool measures both terms on one GPU at P = N x 65 536:
+A rank varies only the offspring rows it needs (sharded variation,
+evolve.DeviceGA.shard_vary).  This tool measures both terms on one GPU at
+P = N x 65 536:
   * per-shard evaluation: after each DeviceGA generation, the shard of every
     rank is evaluated ON ITS OWN (the same rows, schedule and hall of fame a
     rank would play; one launch each, HIP events): the slowest shard sets the
     generation's pace at N (the straggler term), the mean is what N = 1 pays;
-  * replicated work: the generation's wall time minus its evaluation (the
-    fused step's own events) at P = N x 65 536, and the same at 65 536;
+  * replicated work: the one-GPU generation's wall time minus its
+    evaluation (the fused step's own events) at 65 536, plus the critical
+    path of a rank's non-evaluation ops at P = N x 65 536 (op by op, sharded
+    variation) beyond the same ops at 65 536;
 and prints the projected efficiency (N=1 generation time) / (N generation time)
 with t_N = max-shard eval + replicated(P) + all-gather(P) and t_1 = mean-shard
 eval + replicated(65 536).  The all-gather (fitness f64 + lineage f32 per row)
@@ -82,12 +86,14 @@ def shard_evals(ga, n_shards):
     return ms
 
 
-def replicated_ops(ga, reps=3):
-    """Device ms of the work every rank repeats for the whole population, one
-    op at a time on the GA's current state (HIP events, median of reps):
-    merge of P fitness values, the hall-of-fame candidates' prepare (hashes,
-    ranks), selTournament by rank sampling, varAnd of P offspring rows, the
-    clones' inherited fitness, the new members' commit; and the host scan."""
+def replicated_ops(ga, n_shards=1, reps=3):
+    """Device ms of a rank's generation work outside its evaluation, one op at
+    a time on the GA's current state (HIP events, median of reps): merge of P
+    fitness values, selTournament by rank sampling, varAnd (n_shards > 1:
+    sharded variation -- shard 0's rows, then the completion: the candidates'
+    and the next parents' pairs marked and varied, evolve.DeviceGA._complete),
+    the clones' inherited fitness, the hall-of-fame candidates' prepare
+    (hashes, ranks), the new members' commit; and the host scan."""
     P, dev = ga.P, ga.device
     out = {}
 
@@ -116,8 +122,30 @@ def replicated_ops(ga, reps=3):
     chosen = torch.empty(P, dtype=torch.int32, device=dev)
     timed("select_ranked", lambda: D.select_ranked(fit, P, ga.tournsize, ga.seed, 99, ga.ws, chosen=chosen))
     offspring = ga.spare[ga.H:]
-    timed("vary", lambda: D.vary(ga.population, chosen, ga.G, ga.cxpb, ga.mutpb, ga.alpha, ga.mu, ga.sigma,
-                                 ga.indpb, seed=ga.seed, generation=99, out=offspring))
+    kw = dict(seed=ga.seed, generation=99, out=offspring)
+    args = (ga.population, chosen, ga.G, ga.cxpb, ga.mutpb, ga.alpha, ga.mu, ga.sigma, ga.indpb)
+    if n_shards == 1:
+        timed("vary", lambda: D.vary(*args, **kw))
+    else:
+        pairs = (P + 1) // 2
+        hi = P // n_shards
+        skip = (0, (hi + 1) >> 1)
+        shard = torch.zeros(pairs, dtype=torch.uint8, device=dev)
+        shard[skip[0]:skip[1]] = 1
+        timed("vary", lambda: D.vary(*args, **kw, pair_mask=shard))
+        cmask = torch.empty(pairs, dtype=torch.uint8, device=dev)
+        pmask = torch.empty(pairs, dtype=torch.uint8, device=dev)
+        inv = torch.empty(P, dtype=torch.uint8, device=dev)
+
+        def complete(mask, rows, exclude=None):
+            mask.zero_()
+            D.mark_pairs(mask, rows, skip=skip, exclude=exclude)
+            D.vary(*args, **kw, pair_mask=mask, invalid=inv)
+        timed("complete_cand", lambda: complete(cmask, cand[:k]))
+        timed("complete_parents", lambda: complete(pmask, chosen, cmask))
+        out["complete_cand_pairs"] = int(cmask.sum().item())
+        out["complete_parent_pairs"] = int(pmask.sum().item())
+        out["distinct_parents"] = int(torch.unique(chosen).numel())
     inherited = torch.empty(P, dtype=torch.float64, device=dev)
     lin = torch.empty(P, dtype=torch.float32, device=dev)
     timed("inherit", lambda: D.inherit(chosen, fit, inherited, ga.lineage_frames, lin))
@@ -141,8 +169,14 @@ def replicated_ops(ga, reps=3):
         dst = torch.empty((m, ga.G), dtype=ga.dtype, device=dev)
         timed("hof_commit", lambda: D.hof_commit(dst, ga.store, ga.population, cand[:k], src_d, old_n, ga.G,
                                                  ga.hof_hash, ch, hh, nf_d, hf))
-    dev_serial = out.get("merge", 0) + out.get("hof_prepare", 0) + out.get("hof_commit", 0)
-    overlapped = max(out["select_ranked"] + out["vary"] + out["inherit"], out.get("hof_scan_host", 0.0))
+    # on the critical path: merge, the candidates' completion (sharded), their
+    # prepare and commit; the selection, the parents' completion, the shard's
+    # variation and inheritance run on the side stream beside the host scan
+    # (evolve.py)
+    dev_serial = (out.get("merge", 0) + out.get("complete_cand", 0) + out.get("hof_prepare", 0)
+                  + out.get("hof_commit", 0))
+    side = out["select_ranked"] + out.get("complete_parents", 0) + out["vary"] + out["inherit"]
+    overlapped = max(side, out.get("hof_scan_host", 0.0))
     out["replicated_critical_ms"] = dev_serial + overlapped
     return out
 
@@ -160,6 +194,9 @@ def main():
     t1 = timed_steps(ga1, gens)
     res["p65536_wall_ms"] = [w for w, _ in t1]
     res["p65536_eval_ms"] = [e for _, e in t1]
+    ops1 = replicated_ops(ga1, 1)
+    print(json.dumps({"replicated_ops_p65536": ops1}), flush=True)
+    res["replicated_ops_p65536"] = ops1
     del ga1
     torch.cuda.empty_cache()
     # the N-GPU population on one GPU
@@ -174,14 +211,14 @@ def main():
         sh = shard_evals(gaN, N)
         shards.append(sh)
         print(json.dumps({"gen": gaN.generation, "wall_ms": w, "eval_ms": e, "shard_ms": sh}), flush=True)
-    ops = replicated_ops(gaN)
+    ops = replicated_ops(gaN, N)
     print(json.dumps({"replicated_ops_pN": ops}), flush=True)
     res["replicated_ops_pN"] = ops
     repl1 = float(np.median([w - e for w, e in t1]))
-    # a rank at N repeats the population-wide ops of P = N x 65 536 where the
-    # one-GPU run pays them for 65 536, and its shard-sized work (evaluation
-    # prep, order, scatter) as at N = 1
-    replN = repl1 + ops["replicated_critical_ms"] * (1.0 - 1.0 / N)
+    # a rank at N pays the one-GPU generation's non-evaluation time plus what
+    # its P = N x 65 536 ops (sharded variation) cost beyond the same ops at
+    # 65 536; its shard-sized work (evaluation prep, order, scatter) as at N = 1
+    replN = repl1 + max(0.0, ops["replicated_critical_ms"] - ops1["replicated_critical_ms"])
     res["replicated_ms_pN_wall"] = float(np.median([w - e for w, e in zip(walls, evals)]))
     shard_max = float(np.median([max(s) for s in shards]))
     shard_mean = float(np.median([float(np.mean(s)) for s in shards]))
