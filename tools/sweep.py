@@ -27,7 +27,10 @@ def one(args):
     ev = Evaluator(shape, device=dev, group_lanes=args.lane, kernel=args.kernel,
                    dtype=torch.float64 if args.dtype == "f64" else torch.float32)
     gen = torch.Generator(device=dev).manual_seed(1234)
-    genomes = (torch.randn((n, ev.genes), generator=gen, dtype=torch.float64, device=dev) * args.sigma).to(ev.dtype)
+    if args.dist == "uniform":  # toolbox.attr_float = random.random (ga.py:85): bench.py --dist init
+        genomes = torch.rand((n, ev.genes), generator=gen, dtype=torch.float64, device=dev).to(ev.dtype)
+    else:
+        genomes = (torch.randn((n, ev.genes), generator=gen, dtype=torch.float64, device=dev) * args.sigma).to(ev.dtype)
     hof = genomes[:H].contiguous()
     kind, opp, mult = ev.selfplay_schedule(n, H)
     res, _ = ev.evaluate(genomes, kind, opp, mult, opponents=hof)
@@ -48,6 +51,7 @@ def one(args):
         probe = [int(c[13]), int(c[14]), int(c[15])]  # PG_START_PROBE build: start cycles, wave cycles, waves
     mean = sum(ms) / len(ms)
     print(json.dumps({"lib": os.path.basename(os.environ.get("PONG_GA_LIB", "default")), "lanes": args.lane,
+                      "dist": args.dist,
                       "kernel": args.kernel,
                       "shape": shape, "kernel_ms": mean, "min_ms": min(ms), "env_steps": steps,
                       "env_steps_per_s": steps / (mean / 1e3), "fwd": fwd, "f64_redecide": slow,
@@ -67,6 +71,7 @@ def main():
     p.add_argument("--shape", default="6,64,3")
     p.add_argument("--sigma", type=float, default=3.0)
     p.add_argument("--dtype", default="f64")
+    p.add_argument("--dist", default="normal", choices=("normal", "uniform"))
     p.add_argument("--kernel", default="split")
     p.add_argument("--one", action="store_true")
     p.add_argument("--lane", type=int, default=0)
@@ -81,7 +86,7 @@ def main():
                 env["PONG_GA_LIB"] = os.path.abspath(lib)
             cmd = [sys.executable, __file__, "--one", f"--lane={lane}", "--reps", str(args.reps),
                    "--pop", str(args.pop), "--shape", args.shape, "--sigma", str(args.sigma), "--dtype", args.dtype,
-                   "--kernel", args.kernel]
+                   "--kernel", args.kernel, "--dist", args.dist]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 print(json.dumps({"lib": lib, "lanes": lane, "error": r.stderr[-800:]}), flush=True)
