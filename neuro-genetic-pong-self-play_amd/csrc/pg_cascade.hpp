@@ -730,48 +730,41 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-template <int O, typename WT>
-__device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int *k, int lane) {
-  constexpr double kEps = 1.1102230246251565e-16;  // 2^-53
-  double x[6];
+// One lane's hidden unit j in f64 (inputs x, weights w1[0..5], bias w1[6]):
+// its sigmoid and the unit's share of fast_f64_decide's error bound, 4 A_j + 84.
+__device__ __forceinline__ void f64_unit(const double *x, const double *w1, int b, double &sj, double &aj) {
+  double a = b ? w1[6] : 0.0;
+  double A = fabs(a);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    a = fma(w1[i], x[i], a);
+    A = fma(fabs(w1[i]), x[i], A);
+  }
+  // the compact sigmoid (pow(e_d, -a) as exp(-a)(1 + a delta), ~1-2 ulp; the
+  // bound above allows 6): no table load on the service's critical path
+  double tq = pg_exp_f64(-a);
+  if (tq < INFINITY) tq = fma(tq, a * 5.318237706605891e-17, tq);
+  sj = 1.0 / (1.0 + tq);
+  aj = 4.0 * A + 84.0;
+}
+
+__device__ __forceinline__ void f64_features(const int *k, double *x) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) x[i] = __dmul_rn(0.5, (double)k[i]) / 160.0;
-  const int cols = 6 + b;
-  const WT *v = g + (long)H * cols;
-  double zp[O], ep[O];
-#pragma unroll
-  for (int o = 0; o < O; ++o) { zp[o] = 0.0; ep[o] = 0.0; }
-#pragma unroll 1
-  for (int j = lane; j < H; j += 64) {
-    const WT *row = g + (long)j * cols;
-    double a = b ? (double)row[6] : 0.0;
-    double A = fabs(a);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const double w = (double)row[i];
-      a = fma(w, x[i], a);
-      A = fma(fabs(w), x[i], A);
-    }
-    // the compact sigmoid (pow(e_d, -a) as exp(-a)(1 + a delta), ~1-2 ulp; the
-    // bound above allows 6): no table load on the service's critical path
-    double tq = pg_exp_f64(-a);
-    if (tq < INFINITY) tq = fma(tq, a * 5.318237706605891e-17, tq);
-    const double sj = 1.0 / (1.0 + tq);
-#pragma unroll
-    for (int o = 0; o < O; ++o) {
-      const double w2 = (double)v[(long)o * (H + b) + j];
-      zp[o] = fma(w2, sj, zp[o]);
-      ep[o] = fma(fabs(w2), 4.0 * A + 84.0, ep[o]);
-    }
-  }
+}
+
+// fast_f64_decide's decision from the lanes' partial output sums zp and bound
+// sums ep (any lane order: e covers it) and the output biases c.
+template <int O>
+__device__ int f64_decide_sums(const double *zp, const double *ep, const double *c, int lane) {
+  constexpr double kEps = 1.1102230246251565e-16;  // 2^-53
   double z[O], e[O];
 #pragma unroll
   for (int o = 0; o < O; ++o) {
-    const double t = wave_sum_f64(zp[o]);  // any order: e covers it
+    const double t = wave_sum_f64(zp[o]);
     const double u = wave_sum_f64(ep[o]);
-    const double c = b ? (double)v[(long)o * (H + b) + H] : 0.0;
-    z[o] = t + c;
-    e[o] = 2.0 * kEps * (u + 2.0 * fabs(c)) * 1.001 + 1e-300;
+    z[o] = t + c[o];
+    e[o] = 2.0 * kEps * (u + 2.0 * fabs(c[o])) * 1.001 + 1e-300;
   }
   // m-intervals: lanes 0..2O-1 each evaluate one endpoint (z -/+ e)
   constexpr int kBig = 0x7fffffff;  // below the plateau regime
@@ -820,6 +813,79 @@ __device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int
     if (ok) return w;
   }
   return -1;
+}
+
+template <int O, typename WT>
+__device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int *k, int lane) {
+  double x[6];
+  f64_features(k, x);
+  const int cols = 6 + b;
+  const WT *v = g + (long)H * cols;
+  double zp[O], ep[O], c[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) { zp[o] = 0.0; ep[o] = 0.0; }
+#pragma unroll 1
+  for (int j = lane; j < H; j += 64) {
+    const WT *row = g + (long)j * cols;
+    double w1[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w1[i] = (i < 6 || b) ? (double)row[i] : 0.0;
+    double sj, aj;
+    f64_unit(x, w1, b, sj, aj);
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      const double w2 = (double)v[(long)o * (H + b) + j];
+      zp[o] = fma(w2, sj, zp[o]);
+      ep[o] = fma(fabs(w2), aj, ep[o]);
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < O; ++o) c[o] = b ? (double)v[(long)o * (H + b) + H] : 0.0;
+  return f64_decide_sums<O>(zp, ep, c, lane);
+}
+
+// fast_f64_decide for up to kB requests at once (H <= 64: lane j holds hidden
+// unit j of every request): every request's weights are requested before any
+// arithmetic, then the kB decisions run as independent chains -- the service
+// wave's throughput when requests queue (out[q] = -1 where !need[q]).
+template <int O, typename WT, int kB>
+__device__ __forceinline__ void fast_f64_decide_batch(const WT *const *g, const int (*k)[6], const bool *need, int H,
+                                                      int b, int lane, int *out) {
+  const int cols = 6 + b;
+  const bool on = lane < H;
+  const int j = on ? lane : 0;  // lanes past H read unit 0 and contribute nothing
+  double w1[kB][7], w2[kB][O], c[kB][O];
+#pragma unroll
+  for (int q = 0; q < kB; ++q) {
+    if (need[q]) {
+      const WT *row = g[q] + (long)j * cols;
+      const WT *v = g[q] + (long)H * cols;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) w1[q][i] = (i < 6 || b) ? (double)row[i] : 0.0;
+#pragma unroll
+      for (int o = 0; o < O; ++o) {
+        w2[q][o] = (double)v[(long)o * (H + b) + j];
+        c[q][o] = b ? (double)v[(long)o * (H + b) + H] : 0.0;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kB; ++q) {
+    out[q] = -1;
+    if (need[q]) {
+      double x[6];
+      f64_features(k[q], x);
+      double sj, aj;
+      f64_unit(x, w1[q], b, sj, aj);
+      double zp[O], ep[O];
+#pragma unroll
+      for (int o = 0; o < O; ++o) {
+        zp[o] = on ? w2[q][o] * sj : 0.0;
+        ep[o] = on ? fabs(w2[q][o]) * aj : 0.0;
+      }
+      out[q] = f64_decide_sums<O>(zp, ep, c[q], lane);
+    }
+  }
 }
 
 // the six doubled-centroid features, each in [0, 512), as one 54-bit key

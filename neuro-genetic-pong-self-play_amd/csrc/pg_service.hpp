@@ -18,6 +18,11 @@
 
 namespace pg {
 
+// requests the service wave decides together (fast_f64_decide_batch)
+#ifndef PG_SVC_BATCH
+#define PG_SVC_BATCH 4
+#endif
+
 // Every network a launch plays, once, in the layout a game lane holds it
 // (load_net_pk: pre-scaled f32 weights, the left paddle's x-flip folded in,
 // the certificate's bound): record r < n_genomes is entry r's genome as the
@@ -90,6 +95,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 
   if (wave == kSvcGameWaves) {
     // ---------------- service wave: f64 re-decisions for the whole block ----
+    // requests taken together (H <= 64 layouts: one hidden unit per lane)
+    constexpr int kSvcBatch = U * HL <= 64 ? PG_SVC_BATCH : 1;
+    const WT *genomes_svc = (const WT *)p.genomes;
     // An idle poll reads one word (the posted count): the slot scan runs only
     // when it moved.  A request posted after the read moves it again, so the
     // next poll scans once more; the poster's flag store is ordered before
@@ -108,35 +116,68 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         const bool posted = sidx < kSlots && lds_ld(&slots[sidx].flag) == 1;
         unsigned long long mask = __ballot(posted);
         while (mask) {
-          const int sl = base + __builtin_ctzll(mask);
-          mask &= mask - 1;
-          __threadfence_block();
-          const WT *g = (const WT *)slots[sl].g;
-          int k[6];
+          // up to kSvcBatch posted requests at once: the plateau rule on their
+          // f32 outputs, then the certified f64 decision of the rest with all
+          // their weights requested before any arithmetic (fast_f64_decide_batch)
+          int sl[kSvcBatch], idx[kSvcBatch], k[kSvcBatch][6];
+          const WT *g[kSvcBatch];
+          bool need[kSvcBatch];
 #pragma unroll
-          for (int i = 0; i < 6; ++i) k[i] = slots[sl].k[i];
-          float zf[O];
-#pragma unroll
-          for (int o = 0; o < O; ++o) zf[o] = slots[sl].z[o];
-          int idx = plateau_decide<O>(zf, slots[sl].e, lane64);
-          if (idx < 0) idx = fast_f64_decide<O, WT>(g, H, b, k, lane64);
-          // bit 8 / bit 9 of the answer: decided by the numpy-order forward / by the certified one
-          if (idx < 0) {
-            idx = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, k, lds_svc, lane64);
-            if (p.hard_log && lane64 == 0) {
-              const long oo = g - (const WT *)p.opponents;
-              const bool opp = p.opponents != p.genomes && oo >= 0 && oo < (long)p.n_opponents * p.ostride;
-              log_hard(p, (int)(opp ? oo / p.ostride : (g - (const WT *)p.genomes) / p.gstride), opp ? 1 : 0,
-                       idx, 0, k);
+          for (int q = 0; q < kSvcBatch; ++q) {
+            sl[q] = -1;
+            if (mask) {
+              sl[q] = base + __builtin_ctzll(mask);
+              mask &= mask - 1;
             }
-            idx |= 256;
-          } else {
-            idx |= 512;
           }
-          if (lane64 == 0) {
-            slots[sl].idx = idx;
-            __threadfence_block();
-            lds_st(&slots[sl].flag, 2);
+          __threadfence_block();
+#pragma unroll
+          for (int q = 0; q < kSvcBatch; ++q) {
+            need[q] = false;
+            idx[q] = -1;
+            g[q] = genomes_svc;
+            if (sl[q] >= 0) {
+              g[q] = (const WT *)slots[sl[q]].g;
+#pragma unroll
+              for (int i = 0; i < 6; ++i) k[q][i] = slots[sl[q]].k[i];
+              float zf[O];
+#pragma unroll
+              for (int o = 0; o < O; ++o) zf[o] = slots[sl[q]].z[o];
+              idx[q] = plateau_decide<O>(zf, slots[sl[q]].e, lane64);
+              need[q] = idx[q] < 0;
+            }
+          }
+          if constexpr (kSvcBatch > 1) {
+            int f[kSvcBatch];
+            fast_f64_decide_batch<O, WT, kSvcBatch>(g, k, need, H, b, lane64, f);
+#pragma unroll
+            for (int q = 0; q < kSvcBatch; ++q)
+              if (need[q]) idx[q] = f[q];
+          } else {
+            if (need[0]) idx[0] = fast_f64_decide<O, WT>(g[0], H, b, k[0], lane64);
+          }
+#pragma unroll
+          for (int q = 0; q < kSvcBatch; ++q) {
+            if (sl[q] < 0) continue;
+            int d = idx[q];
+            // bit 8 / bit 9 of the answer: decided by the numpy-order forward / by the certified one
+            if (d < 0) {
+              d = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g[q], H, b, k[q], lds_svc, lane64);
+              if (p.hard_log && lane64 == 0) {
+                const long oo = g[q] - (const WT *)p.opponents;
+                const bool opp = p.opponents != p.genomes && oo >= 0 && oo < (long)p.n_opponents * p.ostride;
+                log_hard(p, (int)(opp ? oo / p.ostride : (g[q] - (const WT *)p.genomes) / p.gstride), opp ? 1 : 0,
+                         d, 0, k[q]);
+              }
+              d |= 256;
+            } else {
+              d |= 512;
+            }
+            if (lane64 == 0) {
+              slots[sl[q]].idx = d;
+              __threadfence_block();
+              lds_st(&slots[sl[q]].flag, 2);
+            }
           }
         }
       }

@@ -685,7 +685,8 @@ class DeviceGA:
             # hashes and gathers them); the next selection's parents follow on
             # the side stream (_next_gen_prep), both before generation g + 1's
             # variation overwrites store[H:]
-            cand_pairs = self._complete(g, off, self.population, cand[:k], "cand")
+            # (no hall of fame: the candidates are never read)
+            cand_pairs = self._complete(g, off, self.population, cand[:k] if self.H else cand[:0], "cand")
             self._mark("complete", sub=True)
         # generation g + 1's parents are this offspring; its offspring go to
         # store[H:] (this generation's parents, free now), the buffer the swap
