@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 9
+#define PG_ABI_VERSION 10
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -129,6 +129,12 @@ typedef struct pg_net {
 } pg_net;
 
 typedef struct pg_eval_args {
+  /* ABI 10: sizeof(pg_eval_args) as the caller compiled it.  pg_eval_population
+   * and pg_eval_workspace_bytes refuse any other value (PG_ERR_INVALID / 0
+   * bytes): a binding whose struct is shorter or longer than this header's
+   * would otherwise have the library read past it.  Always the first field,
+   * so even a stale struct's value is read from memory the caller owns. */
+  uint32_t struct_size;
   pg_net net;
   int32_t n_genomes;             /* rows of genomes evaluated by this call (>= 0) */
   int32_t n_games;               /* GAMES_TO_PLAY (config.py:46), 1..64 */

@@ -792,7 +792,16 @@ static size_t split_records_bytes(const pg_eval_args *a) {
          256 * 256;
 }
 
+// ABI 10: the caller's struct must be this header's (pg_eval_args.struct_size)
+static int32_t check_struct_size(const pg_eval_args *a) {
+  if (a->struct_size != sizeof(pg_eval_args))
+    return fail(PG_ERR_INVALID, "pg_eval_args.struct_size=%u, this library's struct is %zu bytes (ABI %d)",
+                a->struct_size, sizeof(pg_eval_args), PG_ABI_VERSION);
+  return PG_OK;
+}
+
 size_t pg_eval_workspace_bytes(const pg_eval_args *a) {
+  if (a && check_struct_size(a) != PG_OK) return 0;
   size_t n = eval_base_workspace(a);
   if (!a) return n;
   const int kernel = resolve_kernel(a);
@@ -810,7 +819,9 @@ int32_t pg_gene_count(const pg_net *net) {
 
 int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   if (!a) return fail(PG_ERR_INVALID, "args is NULL");
-  int32_t rc = check_net(a->net, true);
+  int32_t rc = check_struct_size(a);
+  if (rc != PG_OK) return rc;
+  rc = check_net(a->net, true);
   if (rc != PG_OK) return rc;
   if (a->n_genomes < 0) return fail(PG_ERR_INVALID, "n_genomes=%d < 0", a->n_genomes);
   if (a->n_games < 1 || a->n_games > 64) return fail(PG_ERR_INVALID, "n_games=%d not in [1, 64]", a->n_games);
@@ -1030,6 +1041,7 @@ int32_t pg_decide(const pg_decide_args *a, void *stream) {
 static pg_eval_args wide_decide_eval(const pg_wide_decide_args *a) {
   pg_eval_args e;
   memset(&e, 0, sizeof(e));
+  e.struct_size = sizeof(e);
   e.net = a->net;
   e.n_genomes = a->n;
   e.n_games = 1;

@@ -9,11 +9,19 @@ import sys
 from ._lib import LIB_PATH, PKG_DIR, REPO_DIR
 
 CSRC = os.path.join(PKG_DIR, "csrc")
-# one translation unit per kernel family, compiled in parallel and linked into one .so
-SOURCES = [os.path.join(CSRC, f) for f in ("pong_ga.hip", "pg_wide.hip", "pg_pixels.hip", "pg_service_more.hip",
-                                           "pg_hof.hip", "pg_gen.hip")]
-DEPS = SOURCES + [os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp", "pg_cascade.hpp", "pg_service.hpp")] + [
-    os.path.join(REPO_DIR, "include", "pong_ga.h")]
+HEADERS = [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_eval.hpp", "pg_cascade.hpp",
+                                           "pg_service.hpp")] + [os.path.join(REPO_DIR, "include", "pong_ga.h")]
+# one translation unit per kernel family, compiled in parallel and linked into one .so;
+# pg_service_more.hip is compiled once per (lanes per game, genome type): its ~100
+# k_service instantiations took 10 minutes as one unit
+# (object name, source, extra flags)
+UNITS = [("pong_ga", "pong_ga.hip", []), ("pg_wide", "pg_wide.hip", []), ("pg_pixels", "pg_pixels.hip", []),
+         ("pg_hof", "pg_hof.hip", []), ("pg_gen", "pg_gen.hip", [])] + [
+    (f"pg_service_more_L{L}_{f}", "pg_service_more.hip",
+     [f"-DPG_MORE_L={L}", f"-DPG_MORE_F64={f}"] + (["-DPG_MORE_DISPATCH"] if (L, f) == (8, 1) else []))
+    for L in (8, 16, 32, 64) for f in (1, 0)]
+SOURCES = sorted({os.path.join(CSRC, src) for _, src, _ in UNITS})
+DEPS = SOURCES + [os.path.abspath(__file__)] + HEADERS
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # per-source flags: the iterative ILP machine scheduler makes k_service's frame
 # loop ~5 % faster on the bench than the default (13.57 vs 14.3 ms per launch;
@@ -24,6 +32,19 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # pong_ga.hip instantiates only the bench layout)
 SOURCE_FLAGS = {"pong_ga.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 ARCH = os.environ.get("PG_OFFLOAD_ARCH", "gfx950")
+
+
+def _obj(name: str) -> str:
+    return os.path.join(CSRC, name + ".o")
+
+
+def _stale(obj: str, src: str) -> bool:
+    """An object is rebuilt when it is missing or older than its source, any
+    shared header or this file (headers are not tracked per unit)."""
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in [src, os.path.abspath(__file__)] + HEADERS)
 
 
 def needs_build() -> bool:
@@ -44,17 +65,22 @@ def build(force: bool = False, verbose: bool = False) -> str:
              "-fno-slp-vectorize", "-fPIC",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO_DIR, "include")]
     objs, procs = [], []
-    for src in SOURCES:
-        obj = os.path.join(CSRC, os.path.splitext(os.path.basename(src))[0] + ".o")
-        cmd = [HIPCC] + flags + SOURCE_FLAGS.get(os.path.basename(src), []) + ["-c", "-o", obj, src]
+    # the slow units first, so the parallel build ends sooner
+    for name, src, extra in sorted(UNITS, key=lambda u: not u[0].startswith("pg_service_more")):
+        src = os.path.join(CSRC, src)
+        obj = _obj(name)
+        objs.append(obj)
+        if not force and not _stale(obj, src):
+            continue
+        cmd = [HIPCC] + flags + SOURCE_FLAGS.get(os.path.basename(src), []) + extra + ["-c", "-o", obj + ".tmp", src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        procs.append((subprocess.Popen(cmd), cmd))
-        objs.append(obj)
-    for proc, cmd in procs:
+        procs.append((subprocess.Popen(cmd), cmd, obj))
+    for proc, cmd, obj in procs:
         if proc.wait() != 0:
             raise subprocess.CalledProcessError(proc.returncode, cmd)
-    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", LIB_PATH + ".tmp"] + objs
+        os.replace(obj + ".tmp", obj)
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", LIB_PATH + ".tmp"] + sorted(objs)
     if verbose:
         print(" ".join(link), file=sys.stderr)
     subprocess.check_call(link)

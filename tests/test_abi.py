@@ -153,3 +153,28 @@ def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
             (os.path.join(REPO, "neuro-genetic-pong-self-play_amd"), str(tmp_path / "missing.so")))
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
     assert "refused" in out.stdout and "no CPU fallback" in out.stdout
+
+
+def test_struct_size_refuses_other_layouts(lib):
+    """ABI 10: pg_eval_args.struct_size must be this header's sizeof; a short
+    (or long) struct is refused before any other field is read, and so is the
+    ABI-9 layout, whose first word (net.n_nodes) lands in struct_size."""
+    from pong_amd import _lib
+    a = _lib.PgEvalArgs()
+    assert a.struct_size == ctypes.sizeof(_lib.PgEvalArgs)
+    a.net = _lib.make_net([6, 2, 2])
+    a.n_games, a.n_genomes = 6, 0
+    assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_OK
+    for size in (ctypes.sizeof(_lib.PgEvalArgs) - 8, ctypes.sizeof(_lib.PgEvalArgs) + 8, 0):
+        a.struct_size = size
+        assert lib.pg_eval_population(ctypes.byref(a), None) == _lib.PG_ERR_INVALID
+        assert b"struct_size" in lib.pg_last_error()
+        assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == 0
+
+    class Abi9(ctypes.Structure):  # round 4's layout: no struct_size, ends at horizon
+        _fields_ = [f for f in _lib.PgEvalArgs._fields_ if f[0] != "struct_size"]
+    old = Abi9()
+    old.net = _lib.make_net([6, 64, 3])
+    old.n_games, old.n_genomes = 6, 0
+    rc = lib.pg_eval_population(ctypes.cast(ctypes.byref(old), ctypes.POINTER(_lib.PgEvalArgs)), None)
+    assert rc == _lib.PG_ERR_INVALID and b"struct_size=3" in lib.pg_last_error()

@@ -1,9 +1,11 @@
-"""Build an experiment variant of libpong_ga.so into variants/NAME.so: the
+"""Build an experiment variant of libpong_ga.so into ab/NAME.so: the
 product build's sources and flags (pong_amd/build.py) plus extra defines,
-objects in variants/NAME.obj/ so the product objects stay untouched.
+objects in ab/NAME.obj/ so the product objects stay untouched.  ab/ is
+git-ignored but travels with gpurun (an A/B needs the variant on the box);
+delete it when the A/B is done.
 
     python tools/build_variant.py NAME [-DPG_TIMELINE ...]
-    PONG_GA_LIB=variants/NAME.so python tools/sweep.py ...
+    PONG_GA_LIB=ab/NAME.so python tools/sweep.py ...
 """
 import os
 import subprocess
@@ -16,15 +18,16 @@ from pong_amd import build as B  # noqa: E402
 
 def main(argv):
     name, extra = argv[0], argv[1:]
-    out_dir = os.path.join(REPO, "variants")
+    out_dir = os.path.join(REPO, "ab")
     obj_dir = os.path.join(out_dir, name + ".obj")
     os.makedirs(obj_dir, exist_ok=True)
     flags = [f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(B.REPO_DIR, "include")] + extra
     procs, objs = [], []
-    for src in B.SOURCES:
-        obj = os.path.join(obj_dir, os.path.splitext(os.path.basename(src))[0] + ".o")
-        cmd = [B.HIPCC] + flags + B.SOURCE_FLAGS.get(os.path.basename(src), []) + ["-c", "-o", obj, src]
+    for uname, src, uflags in B.UNITS:
+        src = os.path.join(B.CSRC, src)
+        obj = os.path.join(obj_dir, uname + ".o")
+        cmd = [B.HIPCC] + flags + B.SOURCE_FLAGS.get(os.path.basename(src), []) + uflags + ["-c", "-o", obj, src]
         procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
     for p, cmd in procs:
