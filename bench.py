@@ -428,7 +428,7 @@ def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
     max_rows = max(8, min(max_rows, (1 << 30) // row_bytes))
     per_worker = max(2, min(64, (16 << 20) // row_bytes))
     chunk = max(1, min(chunk, (64 << 20) // row_bytes))
-    genomes = ga.population[lo:lo + max_rows].double().cpu().numpy()
+    genomes = ga.shard_rows()[:max_rows].double().cpu().numpy()
     n = genomes.shape[0]
     kind, opp, mult = D.schedule(ga.schedule, n, ga.n_games, lo, ga.hof_fitness, ga.hof_n, ga.seed,
                                  ga.generation + 1, ga.device)

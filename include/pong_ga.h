@@ -102,8 +102,9 @@ typedef enum pg_kernel {
   PG_KERNEL_RESIDENT = 2,  /* retired (round 4): PG_ERR_UNSUPPORTED */
   PG_KERNEL_SPLIT = 3      /* [6, H<=256, 2..4]: half a lane group per paddle's network, plus one
                               f64 service wave per 1024-thread block for re-decisions */,
-  PG_KERNEL_WIDE = 4,      /* [6, H1<=512, H2<=512, 1..4], n_games <= 8: one 512-thread workgroup per
-                              genome plays its games in lockstep and streams W2 from HBM each frame
+  PG_KERNEL_WIDE = 4,      /* [6, H1<=512, H2<=512, 1..4]: one 512-thread workgroup per genome plays its
+                              games (up to 6; more: balanced chunks of <= 6, one workgroup pass each)
+                              in lockstep and streams W2 from HBM each frame
                               (numpy_nn's f64 order; AUTO picks it for H1 or H2 >= 64) */
   PG_KERNEL_STAGED = 5     /* retired (round 4): PG_ERR_UNSUPPORTED */
 } pg_kernel;
@@ -190,7 +191,8 @@ typedef struct pg_eval_args {
                                     device needs no host round trip before the launch. */
   int32_t prep;                  /* pg_prep (ABI 7): PG_PREP_ALL unless the records are prepared in two calls */
   int32_t horizon;               /* ABI 8, SURVEY 8(d)'s fixed-horizon measurement mode; 0 = off (evaluate()'s
-                                    episodes).  T > 0 (SPLIT kernel, [6, <=64, 3] networks only): every game slot
+                                    episodes).  T > 0 (SPLIT kernel only: [6, 33..64, 3] networks, the default
+                                    8-lane groups, untraced; else PG_ERR_UNSUPPORTED): every game slot
                                     runs exactly T frames; an episode that terminates (main.py:102-107) before
                                     frame T is scored (calculate_reward) and the slot auto-resets (a fresh
                                     episode, the same networks, the serve sequence continuing), the partial

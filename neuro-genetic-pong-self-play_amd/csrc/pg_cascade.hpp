@@ -521,10 +521,12 @@ __device__ __forceinline__ int group_broadcast(int v, int leader_lane) {
 // ================================================ split-lane helpers ==
 template <int L>
 __device__ __forceinline__ int other_half(int v) {
+  // (every lane reads a valid source lane, so the old value is never kept: no
+  // v_mov of a zero ahead of the DPP move)
   if constexpr (L == 8) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror: i <-> 7-i
+    return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);  // row_half_mirror: i <-> 7-i
   } else if constexpr (L == 16) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror: i <-> 15-i
+    return __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);  // row_mirror: i <-> 15-i
   } else if constexpr (L == 32) {
     const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
     return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
@@ -584,10 +586,13 @@ struct SlowSlot {
   int memo_idx[kMemo];
   uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
   int rally_at, rally_span;
-  // fixed-horizon mode (pg_eval_args.horizon; side-0 slot): the completed
-  // episodes' reward sum, count and ZeroDivisionError flag, every episode's points
-  double hz_sum;
-  int hz_eps, hz_s1, hz_s2, hz_zd;
+};
+
+// fixed-horizon mode (pg_eval_args.horizon), one per game group: the completed
+// episodes' reward sum, count and ZeroDivisionError flag, every episode's points
+struct HorizonSlot {
+  double sum;
+  int eps, s1, s2, zd;
 };
 
 // The plateau certificate in f32, tried by the game wave itself where

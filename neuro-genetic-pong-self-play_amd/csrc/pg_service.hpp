@@ -18,9 +18,11 @@
 
 namespace pg {
 
-// requests the service wave decides together (fast_f64_decide_batch)
+// requests the service wave decides together (fast_f64_decide_batch).  1 in
+// the product: batches of 4 measured neutral (profiles/r04/sweep_svc_batch_a6.log)
+// and their arrays count against every wave's register allocation (round-5 review)
 #ifndef PG_SVC_BATCH
-#define PG_SVC_BATCH 4
+#define PG_SVC_BATCH 1
 #endif
 
 // Every network a launch plays, once, in the layout a game lane holds it
@@ -59,6 +61,30 @@ __global__ __launch_bounds__(256) void k_prep_records(EvalParams p) {
   store_rec<U, O>(n, p.recs + (net * HL + hl) * F);
 }
 
+#ifdef PG_PROBE_EXTRA
+// Timing-only experiment (tools/runs/r5_b2.sh): N independent instructions of
+// one class per visible frame, writing a dummy register from live inputs, so
+// the games play exactly as in the product and the launch time's change is the
+// in-situ issue cost of that class.  Modes: 1 v_rcp_f32 x16, 2 v_exp_f32 x16,
+// 3 v_pk_fma_f32 x24, 4 v_fma_f32 x48, 5 v_add_u32 x24,
+// 7 v_mov_b32 x24, 8 v_pk_add_f32 x24, 9 v_add_f32 x48.
+template <int M>
+__device__ __forceinline__ void pg_probe_extra(float2v w, float2v w2, float a, float b, float &v, float2v &pp,
+                                               int &sv) {
+#pragma unroll
+  for (int r = 0; r < (M == 4 || M == 9 ? 48 : (M <= 2 ? 16 : 24)); ++r) {
+    if constexpr (M == 1) asm volatile("v_rcp_f32 %0, %1" : "=v"(v) : "v"((r & 1) ? a : b));
+    if constexpr (M == 2) asm volatile("v_exp_f32 %0, %1" : "=v"(v) : "v"((r & 1) ? a : b));
+    if constexpr (M == 3) asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(pp) : "v"(w), "v"(w2), "v"((r & 1) ? w : w2));
+    if constexpr (M == 4) asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(v) : "v"(a), "v"(b), "v"((r & 1) ? a : b));
+    if constexpr (M == 5) asm volatile("v_add_u32 %0, %1, %2" : "=v"(v) : "v"(a), "v"(b));
+    if constexpr (M == 7) asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"((r & 1) ? a : b));
+    if constexpr (M == 8) asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(pp) : "v"(w), "v"((r & 1) ? w : w2));
+    if constexpr (M == 9) asm volatile("v_add_f32 %0, %1, %2" : "=v"(v) : "v"(a), "v"((r & 1) ? a : b));
+  }
+}
+#endif
+
 // kUntraced: a launch without a trace buffer (the GA's), the trace tests
 // compiled out of the frame instead of tested on p.trace every frame.
 // kHorizon: SURVEY 8(d)'s fixed-horizon measurement mode (pg_eval_args.horizon,
@@ -71,6 +97,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   constexpr int HL = L / 2;
   constexpr int kSlots = kSvcGameWaves * (64 / L) * 2;
   __shared__ SlowSlot slots[kSlots];
+  // fixed-horizon bookkeeping, one per game group (kHorizon instances only)
+  __shared__ HorizonSlot hz[kHorizon ? kSlots / 2 : 1];
   __shared__ int waves_done;
   __shared__ int posted;  // requests posted so far (the service wave polls this one word)
   // every serve of every game slot (Pong::serve_entry is a function of the
@@ -198,7 +226,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 
   NetP<U, O> net;
   Pong st;
-  int kind = 0, act_r = 0, act_l = 0, timeout = 0, total = 0, frames = 0, tab_off = 0;
+  // Frame bookkeeping against a wave-scalar frame counter (every lane of the
+  // loop steps one frame per iteration): a game's frames = sframe - fstart, its
+  // no-score counter (main.py:128-135) = sframe - (tend - TIMEOUT_THRESH), so a
+  // plain frame updates neither; total (main.py:73) and the score-based end
+  // (main.py:102-107) change only at a point, inside the rare block
+  int kind = 0, act_r = 0, act_l = 0, total = 0, fstart = 0, tend = 0, c_vis = 0, tab_off = 0;
+  int sframe = 0;
   const WT *gm = genomes;
   uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0, hidden = 0;
 
@@ -211,6 +245,15 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   }
   bool fresh = true;
   bool w_scripted = true, w_onep = true;  // wave-uniform; set at the first frame's starts
+  // wave-uniform: some game of the wave starts, or has a hidden ball whose serve
+  // delay the top block advances; set where that can change (the top block, the
+  // rare block), so a plain frame tests one scalar
+  bool top = true;
+#ifdef PG_PROBE_EXTRA
+  float probe_v = 0.f;
+  float2v probe_p = float2v{0.f, 0.f};
+  int probe_s = 0;
+#endif
 #ifdef PG_START_PROBE  // diagnostic build: shader cycles of the game-start blocks vs the wave's total
   uint64_t probe_fresh = 0;
   const uint64_t probe_t0 = __builtin_amdgcn_s_memtime();
@@ -232,8 +275,14 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     const uint64_t probe_f0 = __builtin_amdgcn_s_memtime();
 #endif
     PG_PP(pp_frames, true);
-    // a game start or a hidden ball: one wave-uniform test on the common path
-    if (PG_ANY(fresh || !st.vis)) {
+    sframe += 1;
+#ifdef PG_TIMELINE
+    constexpr bool kJumps = !kHorizon;
+#else
+    const bool kJumps = !kHorizon && (kUntraced || p.trace == nullptr);  // the serve delay advanced at once
+#endif
+    // a game start or a hidden ball: one wave-uniform scalar test on the common path
+    if (top) {
     if (fresh) {  // start game w (genome-major: the 6 games of a genome are adjacent)
       const int i = w / p.n_games;
       const int g = w - i * p.n_games;
@@ -247,16 +296,21 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       gm = nn ? opponents + (long)oj * p.ostride : gr;
       load_rec<U, O>(net, p.recs + ((nn ? (long)p.n_genomes + oj : (long)i) * HL + hl) * rec_floats<U, O>());
       st.reset(0, kind == kOppRomCpu);
-      if (!tabbed) st.seed = game_seed(p.seed, g);  // (a wave-uniform test)
+      // the slot's serve seed: the LDS table holds a tabbed slot's first
+      // kServeTabPoints serves; a horizon slot carries its point count across
+      // auto-resets past them, where the step falls back to serve_entry(seed, pt)
+      if (kHorizon || !tabbed) st.seed = game_seed(p.seed, g);  // (a wave-uniform test)
       tab_off = g * kServeTabPoints;
-      act_r = act_l = total = frames = 0;
-      timeout = -1;  // frame 1 does not count (main.py:94-96): it takes the counter to 0
+      act_r = act_l = total = c_vis = 0;
+      fstart = sframe - 1;             // this iteration is the game's frame 1
+      tend = sframe + kTimeoutThresh;  // frame 1 does not count (main.py:94-96): it takes the counter to 0
       fresh = false;
       if (hl == 0) slots[sx].n_memo = 0;
       if (lig == 0) slots[sx].rally_at = -1;  // (sx is the side-0 slot there)
       if (kHorizon && lig == 0) {
-        slots[sx].hz_sum = 0.0;
-        slots[sx].hz_eps = slots[sx].hz_s1 = slots[sx].hz_s2 = slots[sx].hz_zd = 0;
+        const int gx = threadIdx.x / L;
+        hz[gx].sum = 0.0;
+        hz[gx].eps = hz[gx].s1 = hz[gx].s2 = hz[gx].zd = 0;
       }
 #ifdef PG_TIMELINE  // experiment build: per-game wall-clock start/end into p.trace
       t_start = wall_clock64();
@@ -274,22 +328,17 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // once -- the same state, actions, timeout and frame counts as stepping
     // them (never while tracing, which records every frame).
     {
-#ifdef PG_TIMELINE
-      constexpr bool kTrace = false;
-#else
-      const bool kTrace = !kUntraced && p.trace != nullptr;
-#endif
       const bool hid = !st.vis && st.timer >= 2;
       PG_PP(pp_hidden, hid);
-      if (!kTrace && !kHorizon && hid) {
+      if (kJumps && hid) {
         const int h = st.timer - 1;
         st.rpy = Pong::drift(st.rpy, h);
         if (!st.one_player) st.lpy = Pong::drift(st.lpy, h);
         st.timer = 1;
         act_r = clamp_action(paddle_c2(st.rpy), 0);
         act_l = clamp_action(paddle_c2(st.lpy), 0);
-        timeout += h;
-        frames += h;
+        fstart -= h;  // frames += h, and the no-score counter with them
+        tend -= h;
         hidden += h;
       }
     }
@@ -298,6 +347,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // 1-player env (both fixed for a game; no per-frame test otherwise)
     w_scripted = PG_ANY(kind != kOppNN);
     w_onep = PG_ANY(st.one_player != 0);
+    top = false;  // every start and serve delay above is done
     }
     const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
 #ifdef PG_PATH_PROBE
@@ -308,7 +358,6 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     }, w_onep);
     const bool bounced = ev == kStepBounce;  // a paddle returned the ball this frame
     PG_PP(pp_face, ev != kStepFly || st.hits != hits_b || st.point != pt_b);
-    frames += 1;
     const int vis = st.vis;
     const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
     const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
@@ -323,6 +372,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #pragma unroll
       for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
       int idx = certify_c<O>(z, net.ct);
+#ifdef PG_PROBE_EXTRA  // timing-only experiment build: extra instructions of one class every visible frame
+      pg_probe_extra<PG_PROBE_EXTRA>(net.w1[0][0], net.w1[1][1], z[0], z[1], probe_v, probe_p, probe_s);
+#endif
       const bool left_nn = kind == kOppNN;
       if (side && !left_nn) idx = 0;  // the left half is idle against a scripted opponent
 #ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
@@ -393,20 +445,19 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         left = hardcoded(by2, lc2);
         if (kind == kOppScore && st.s1 > st.s2) left = 0;
       }
-      c_fwd += left_nn ? 2 : 1;
+      c_vis += 1;  // forwards: c_vis x (1 or 2 networks), counted at the game's end
     }
     act_l = clamp_action(lc2, left);
     act_r = clamp_action(rc2, right);
 #ifndef PG_TIMELINE
     if (!kUntraced && p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
+      const int frames = sframe - fstart;
       if (w < p.trace_games && frames <= p.trace_cap && lig == 0)
         p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
     }
 #endif
     // calculate_timeout_and_frames (main.py:128-135); at most one point a frame
     const bool same = ev != kStepPoint;  // a miss grows exactly one score
-    total += same ? 0 : timeout;
-    timeout = same ? timeout + 1 : 0;
 #ifndef PG_NO_RALLY_SKIP
     // a periodic rally ends at the timeout with nothing else changed: jump there
     // (never while tracing, which records every frame's actions)
@@ -427,18 +478,25 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // opening at the 8th return instead of at timeout 256, with a 64-frame
     // first span, fires at the cycle's first repetition in the common
     // two-bounce rally (tools/long_games.py: 460 instead of 610 frames).
-    const bool rally_check = !kTracing && !kHorizon && bounced && st.hits >= kRallyHits && timeout <= kTimeoutThresh;
+    const bool rally_check = !kTracing && !kHorizon && bounced && st.hits >= kRallyHits;
 #else
     constexpr bool rally_check = false;
 #endif
     PG_PP(pp_rally, rally_check);
-    bool over = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh;
-    if constexpr (kHorizon) over = over || frames >= p.horizon;
+    // the no-score counter past TIMEOUT_THRESH (main.py:102-107); the scores end a game only at a point
+    bool over = sframe > tend;
+    if constexpr (kHorizon) over = over || sframe - fstart >= p.horizon;
     // a point, a rally check or a game end: one wave-uniform test on the common path
     if (PG_ANY(!same || rally_check || over)) {
-    if (!same && lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
+    if (!same) {  // a point: total_frames += timeout, timeout = 0 (main.py:128-135); the scores' end test
+      total += sframe - 1 - (tend - kTimeoutThresh);
+      tend = sframe + kTimeoutThresh;
+      over = over || st.s1 >= kWinScore || st.s2 >= kWinScore || st.done();
+      if (lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
+    }
 #ifndef PG_NO_RALLY_SKIP
-    if (rally_check) {
+    const int timeout = sframe - (tend - kTimeoutThresh);
+    if (rally_check && timeout <= kTimeoutThresh) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
       const uint64_t key = rally_key(st, act_r, act_l);
       const int at = slots[rs].rally_at;
@@ -450,9 +508,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         }
       } else if (slots[rs].rally_key == key) {
         const int rest = kTimeoutThresh + 1 - timeout;
-        frames += rest;
+        fstart -= rest;  // frames += rest; the counter at TIMEOUT_THRESH + 1
         skipped += rest;
-        timeout = kTimeoutThresh + 1;
+        tend = sframe - 1;
       } else if (timeout - at >= slots[rs].rally_span) {
         if (lig == 0) {
           slots[rs].rally_key = key;
@@ -461,28 +519,28 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         }
       }
     }
-    over = over || timeout > kTimeoutThresh;  // a rally jump ends the game
+    over = over || sframe > tend;  // a rally jump ends the game
 #endif
     if constexpr (kHorizon) {
       if (over) {  // an episode's end or the horizon's
-        const int rs = (threadIdx.x / L) * 2;
-        const bool ep_end = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh;
+        const int gx = threadIdx.x / L;
+        const bool ep_end = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || sframe > tend;
         if (lig == 0) {
           if (ep_end) {  // perform_episode's reward (main.py:108-112), summed in episode order
             int zd;
-            slots[rs].hz_sum = __dadd_rn(slots[rs].hz_sum, episode_reward(st, total, p.mult[w], zd));
-            slots[rs].hz_zd |= zd;
-            slots[rs].hz_eps += 1;
+            hz[gx].sum = __dadd_rn(hz[gx].sum, episode_reward(st, total, p.mult[w], zd));
+            hz[gx].zd |= zd;
+            hz[gx].eps += 1;
           }
-          slots[rs].hz_s1 += st.s1;
-          slots[rs].hz_s2 += st.s2;
+          hz[gx].s1 += st.s1;
+          hz[gx].s2 += st.s2;
         }
-        if (ep_end && frames < p.horizon) {  // auto-reset: a fresh episode in the slot, the serves continuing
+        if (ep_end && sframe - fstart < p.horizon) {  // auto-reset: a fresh episode in the slot, the serves continuing
           const int pt = st.point;
           st.reset(st.seed, st.one_player);
           st.point = pt;
           act_r = act_l = total = 0;
-          timeout = -1;
+          tend = sframe + 1 + kTimeoutThresh;  // the next iteration is the episode's frame 1
           over = false;
         }
       }
@@ -490,16 +548,16 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     if (over) {
       if constexpr (kHorizon) {
         if (lig == 0) {
-          const int rs = (threadIdx.x / L) * 2;
-          p.rewards[w] = slots[rs].hz_sum;
-          p.scores[2 * w] = slots[rs].hz_s1;
-          p.scores[2 * w + 1] = slots[rs].hz_s2;
-          p.frames[w] = frames;
-          p.total_frames[w] = (double)slots[rs].hz_eps;
-          p.status_game[w] = slots[rs].hz_zd;
+          const int gx = threadIdx.x / L;
+          p.rewards[w] = hz[gx].sum;
+          p.scores[2 * w] = hz[gx].s1;
+          p.scores[2 * w + 1] = hz[gx].s2;
+          p.frames[w] = sframe - fstart;
+          p.total_frames[w] = (double)hz[gx].eps;
+          p.status_game[w] = hz[gx].zd;
         }
       } else {
-        if (lig == 0) finish_game(p, w, st, frames, total);
+        if (lig == 0) finish_game(p, w, st, sframe - fstart, total);
       }
 #ifdef PG_TIMELINE
       if (p.trace && w < p.trace_games && lig == 0) {
@@ -514,13 +572,16 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         }
       }
 #endif
-      c_steps += frames;
+      c_steps += sframe - fstart;
+      c_fwd += (kind == kOppNN ? 2u : 1u) * (uint32_t)c_vis;
       c_games += 1;
       int ww = 0;
       if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
       w = group_broadcast<L>(ww, leader);
       fresh = true;
     }
+    // what the next frame's top block has to do: a start, or (a point) a serve delay to advance
+    top = PG_ANY(fresh || (kJumps && !st.vis && st.timer >= 2));
     }
   }
   if (p.counters && c_games) {
@@ -553,6 +614,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     atomicAdd((unsigned long long *)&p.counters[14], (unsigned long long)pp_fail);
     atomicAdd((unsigned long long *)&p.counters[15], (unsigned long long)pp_hidden);
   }
+#endif
+#ifdef PG_PROBE_EXTRA  // keep the probe's results alive (never true)
+  if (p.counters && probe_v == 1234.5f && probe_p.x == 1234.5f && probe_s == 1234567) p.counters[15] = 1;
 #endif
   // this wave will post no more requests
   if (lane64 == 0) atomicAdd(&waves_done, 1);

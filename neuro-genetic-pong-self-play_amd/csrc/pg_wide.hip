@@ -6,6 +6,8 @@
 // plays all n_games (6) games of one genome in lockstep, so the genome's W2
 // (the 512 x 513 matrix that is 98 % of the genes) is read once per frame for
 // all six games; each NN opponent's W2 is read once per frame for its game.
+// (More than six games per genome: balanced chunks of at most six, one work
+// item each.)
 // Per frame:
 //   A  wave 0, one lane per game: physics step, centroids, features, the
 //      scripted left paddles; the set of networks that must run this frame
@@ -31,7 +33,7 @@
 namespace pg {
 
 constexpr int kWideThreads = 512;  // = max H2: one W2 row per thread
-constexpr int kWideMaxGames = 8;
+constexpr int kWideMaxGames = 8;  // LDS slots for games (k_wide<NG <= 8>; the product runs NG = 6)
 
 // W2 tiles: kTileRowBytes (K = kTileRowBytes / sizeof(WT) columns) of every
 // row, in kPieces 16-B pieces; a wave's piece load is 64 rows x 16 B = 1 KB.
@@ -305,29 +307,37 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
   const int n_games = p.n_games;
+  // a genome's games in chunks of at most NG: with more than NG games a genome
+  // is ceil(n_games / NG) work items of balanced size, each streaming the
+  // genome's W2 for its own games (the opponents' streams are per game anyway)
+  const int n_chunks = (n_games + NG - 1) / NG;
+  const int chunk = (n_games + n_chunks - 1) / n_chunks;
   const bool probe = p.wide_probe_k != nullptr;  // pg_wide_decide (n_games = 1)
   uint64_t c_streams = 0;
   if (t < NG * 4) cnt[t] = 0;  // (the genome loop's first barrier orders this before any use)
-  const int n_genomes_active = active_genomes(p);
+  const int n_items = active_genomes(p) * n_chunks;
 
-  for (;;) {  // genomes, one per workgroup at a time
+  for (;;) {  // genomes (or chunks of a genome's games), one per workgroup at a time
     const int t = opaque_tid(), lane = t & 63;
     if (t == 0) ctl[0] = (int)atomicAdd(p.work, 1u);
     __syncthreads();
-    const int gi = __builtin_amdgcn_readfirstlane(ctl[0]);  // uniform: the genome loop's exit
-    if (gi >= n_genomes_active) break;
+    const int item = __builtin_amdgcn_readfirstlane(ctl[0]);  // uniform: the genome loop's exit
+    if (item >= n_items) break;
+    const int gi = item / n_chunks;
+    const int g0 = (item - gi * n_chunks) * chunk;  // the item's first game slot
+    const int ng = min(chunk, n_games - g0);
     const int grow = genome_row(p, gi);
     const WT *gbase = genomes + (long)grow * p.gstride;
 
-    // game state: wave 0, lane g < n_games, in LDS between the phases (WideGame)
-    if (wid == 0 && lane < n_games) {
+    // game state: wave 0, lane c < ng (game g0 + c), in LDS between the phases (WideGame)
+    if (wid == 0 && lane < ng) {
       WideGame g;
-      g.w = gi * n_games + lane;
+      g.w = gi * n_games + g0 + lane;
       // probe (pg_wide_decide): one scripted-opponent "game" whose single frame
       // is the genome on the given features
       g.kind = probe ? kOppHard : p.kind[g.w];
       orow[lane] = g.kind == kOppNN ? (long long)p.opp[g.w] * p.ostride : 0;
-      g.st.reset(game_seed(p.seed, lane), g.kind == kOppRomCpu);
+      g.st.reset(game_seed(p.seed, g0 + lane), g.kind == kOppRomCpu);
       g.act_r = g.act_l = g.timeout = g.total = g.frames = 0;
       g.active = 1;
       g.s1b = g.s2b = g.vis = g.lc2 = g.rc2 = g.left = g.pad0 = g.pad1 = 0;
@@ -341,7 +351,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       rat[lane] = -1;  // no rally search open
     }
     if (wid == 0) {
-      const bool nng = lane < n_games && !probe && p.kind[gi * n_games + (lane < n_games ? lane : 0)] == kOppNN;
+      const bool nng = lane < ng && !probe && p.kind[gi * n_games + g0 + (lane < ng ? lane : 0)] == kOppNN;
       const uint64_t nb = __ballot(nng);
       if (lane == 0) ctl[1] = 1 | (int)((unsigned)nb << 1);  // networks to re-lay: bit 0 genome, 1 + c opponents
     }
@@ -353,7 +363,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       int *cf = ctl + 8 + (fno & 1) * 32;  // [0] column mask, [1] any active, [2] nets, [3..] net ids
       // ---- A: env.step + find_stuff + inference features (main.py:77-87)
       if (wid == 0) {
-        const bool mine = lane < n_games;
+        const bool mine = lane < ng;
         WideGame g;
         if (mine) g = wg_load(&games[lane]);
         const bool active = mine && g.active;
@@ -760,7 +770,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
       }
 
       // ---- E: actions, clamp, bookkeeping (main.py:88-107, 128-135)
-      if (wid == 0 && lane < n_games) {
+      if (wid == 0 && lane < ng) {
         WideGame &g = games[lane];  // in place: the fields phase E touches, read and written in LDS
         if (g.active && probe) {
           p.wide_probe_index[gi] = argmax_np(outv, O);
@@ -847,22 +857,26 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
 bool wide_shape_ok(const pg_net &n, int n_games) {
   return n.n_nodes == 4 && n.nodes[0] == 6 && n.nodes[1] >= 1 && n.nodes[1] <= kWideThreads &&
          n.nodes[2] >= 1 && n.nodes[2] <= kWideThreads && n.nodes[3] >= 1 && n.nodes[3] <= 4 &&
-         n_games >= 1 && n_games <= kWideMaxGames;
+         n_games >= 1 && n_games <= 64;
 }
 
-static int wide_groups(int n_games) { return n_games <= 6 ? 6 : 8; }
+// games per work item (k_wide's NG): 6, so GAMES_TO_PLAY = 6 plays a genome's
+// games in one lockstep pass; more games are split into balanced chunks
+// (k_wide<8> spilled 112 VGPRs: round-4 review)
+constexpr int kWideNG = 6;
+static int wide_items(int n_genomes, int n_games) { return n_genomes * ((n_games + kWideNG - 1) / kWideNG); }
 
-static int wide_grid(int n_genomes) {
+static int wide_grid(int n_items) {
   const int cap = num_cus();
-  return n_genomes < cap ? n_genomes : cap;
+  return n_items < cap ? n_items : cap;
 }
 
 size_t wide_workspace_bytes(const pg_eval_args *a) {
   if (!a || a->n_genomes <= 0 || a->net.n_nodes != 4) return 0;
-  const int NG = wide_groups(a->n_games);
+  const int NG = kWideNG;
   const WideLayout l = wide_layout(a->net.nodes[1], a->net.nodes[2], a->net.bias ? 1 : 0,
                                    a->net.dtype == PG_F64 ? 8 : 4);
-  return (size_t)wide_grid(a->n_genomes) * (size_t)(NG + 1) * (size_t)l.net_bytes;
+  return (size_t)wide_grid(wide_items(a->n_genomes, a->n_games)) * (size_t)(NG + 1) * (size_t)l.net_bytes;
 }
 
 template <int NG, typename WT>
@@ -876,7 +890,7 @@ static int32_t launch_wide_t(EvalParams p, void *scratch, hipStream_t s) {
   // above 64 KB of dynamic LDS; an older runtime that rejects the attribute launches anyway
   (void)hipFuncSetAttribute((const void *)k_wide<NG, WT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   (void)hipGetLastError();
-  const int grid = wide_grid(p.n_genomes);  // wide_workspace_bytes sized the scratch for this grid
+  const int grid = wide_grid(wide_items(p.n_genomes, p.n_games));  // wide_workspace_bytes sized the scratch for it
   if (grid <= 0) return PG_OK;
   p.wide_scratch = scratch;
   hipLaunchKernelGGL((k_wide<NG, WT>), dim3(grid), dim3(kWideThreads), (size_t)lds, s, p);
@@ -885,9 +899,8 @@ static int32_t launch_wide_t(EvalParams p, void *scratch, hipStream_t s) {
 }
 
 int32_t launch_wide(const EvalParams &p, int dtype, void *scratch, hipStream_t s) {
-  if (wide_groups(p.n_games) == 6)
-    return dtype == PG_F64 ? launch_wide_t<6, double>(p, scratch, s) : launch_wide_t<6, float>(p, scratch, s);
-  return dtype == PG_F64 ? launch_wide_t<8, double>(p, scratch, s) : launch_wide_t<8, float>(p, scratch, s);
+  return dtype == PG_F64 ? launch_wide_t<kWideNG, double>(p, scratch, s)
+                         : launch_wide_t<kWideNG, float>(p, scratch, s);
 }
 
 }  // namespace pg

@@ -130,6 +130,8 @@ class Evaluator:
         ``horizon`` (pg_eval_args.horizon, default ``self.horizon``): T > 0 runs
         every game slot for exactly T frames with auto-reset (rewards = the
         completed episodes' sum, total_frames = their count; see pong_ga.h).
+        Only the split kernel's bench layout has it: [6, 33..64, 3] networks on
+        the default 8-lane groups, untraced (else PongGAError).
         """
         dev = self.device
         n = genomes.shape[0] if rows is None else rows.shape[0]

@@ -99,7 +99,10 @@ class DeviceGA:
         self._next = None        # (generation, inv, inherited): offspring already varied into spare[H:]
         self.early_prep = True   # _early_prep: schedule + genome records during the hall-of-fame scan
         self.hard_log = None     # optional [cap, 8] int32: the evaluation's hard decisions (pg_eval_args.hard_log)
-        self.on_evaluate = None  # optional callable(g, rows, opponents, result), right after each evaluation
+        # optional callable(g, rows, opponents, result), right after each evaluation; in the fused
+        # path ``rows`` is the whole row buffer, of which (sharded) only this rank's shard
+        # [lo, hi) and the rows result played (result indices -> last_rows) are current
+        self.on_evaluate = None
         # Evaluation order: a genome's longest game sets when its last game ends,
         # and a long game started late sets the launch's tail.  Each row carries
         # the longest game of its lineage's last evaluation (a child inherits its
@@ -134,23 +137,42 @@ class DeviceGA:
 
     # ------------------------------------------------------------ views
     @property
-    def population(self) -> torch.Tensor:
+    def _rows(self) -> torch.Tensor:
+        """Every population row of the device buffer (internal: with sharded
+        variation only this rank's shard, the hall-of-fame candidates and the
+        next parents are current)."""
         return self.store[self.H:]
+
+    @property
+    def population(self) -> torch.Tensor:
+        """The current population [P, G] (the reference's ``ga.population``).
+        With sharded variation (N > 1, ``shard_vary``) a rank holds only its
+        shard's rows current, so this raises instead of returning stale rows:
+        use :meth:`shard_rows` (this rank's rows, no communication) or
+        :meth:`population_full` (a collective)."""
+        if self._sharded():
+            raise RuntimeError("DeviceGA.population: with sharded variation this rank holds only its shard "
+                               "current; use shard_rows() or population_full() (a collective)")
+        return self._rows
+
+    def shard_rows(self) -> torch.Tensor:
+        """This rank's shard of the population, rows [lo, hi) (always current)."""
+        return self._rows[self.lo:self.hi]
 
     def population_full(self) -> torch.Tensor:
         """The whole current population on this rank: ``population`` itself, or
         with sharded variation the ranks' shard rows all-gathered (a
         collective: every rank calls it)."""
         if not self._sharded():
-            return self.population
-        return PD.gather_rows(self.population[self.lo:self.hi].contiguous(), self.P, self.group)
+            return self._rows
+        return PD.gather_rows(self._rows[self.lo:self.hi].contiguous(), self.P, self.group)
 
     def population_hash(self) -> torch.Tensor:
         """pg_row_hash of every population row ([P] int64; sharded: each rank
         hashes its shard and the 8-B hashes are all-gathered)."""
         if not self._sharded():
-            return D.row_hash(self.population, self.G)
-        return PD.gather_rows(D.row_hash(self.population[self.lo:self.hi], self.G), self.P, self.group)
+            return D.row_hash(self._rows, self.G)
+        return PD.gather_rows(D.row_hash(self._rows[self.lo:self.hi], self.G), self.P, self.group)
 
     def _sharded(self) -> bool:
         return bool(self.shard_vary and self.fused and self.world > 1 and dist.is_initialized())
@@ -193,7 +215,7 @@ class DeviceGA:
         if tuple(genomes.shape) != (self.P, self.G):
             raise ValueError(f"genomes must be [{self.P}, {self.G}], got {tuple(genomes.shape)}")
         self._next = None
-        self.population.copy_(genomes.to(device=self.device, dtype=self.dtype))
+        self._rows.copy_(genomes.to(device=self.device, dtype=self.dtype))
         if fitness is None:
             self.valid.zero_()
             self.fitness.zero_()
@@ -398,14 +420,14 @@ class DeviceGA:
 
     def _step_torch(self) -> dict:
         if self.generation < 0:
-            fit = self._evaluate(0, self.population, ~self.valid)
+            fit = self._evaluate(0, self._rows, ~self.valid)
             nevals = int((~self.valid).sum())
             new_fit = torch.where(self.valid, self.fitness, fit)
             self._check(new_fit)
             self.fitness, self.valid = new_fit, torch.ones_like(self.valid)
             # generation 1's offspring go to spare[H:] (no swap after the initial update)
-            self._hof_update(new_fit, self.population, self.spare,
-                             overlap=lambda: self._prefetch(1, self.population, new_fit, self.spare))
+            self._hof_update(new_fit, self._rows, self.spare,
+                             overlap=lambda: self._prefetch(1, self._rows, new_fit, self.spare))
             self.store[: self.hof_n] = self.spare[: self.hof_n]
             self.generation = 0
             return self._record(0, nevals)
@@ -415,7 +437,7 @@ class DeviceGA:
         if self._next is not None and self._next[0] == g:
             inv, inherited = self._next[1:]  # selected and varied during the previous hall-of-fame scan
         else:
-            inv, inherited = self._select_vary(g, self.population, self.fitness, off)
+            inv, inherited = self._select_vary(g, self._rows, self.fitness, off)
         self._next = None
         self._mark("select_vary")
         fit = self._evaluate(g, off, inv)  # invalid_ind only: clones keep their parent's fitness
@@ -658,13 +680,13 @@ class DeviceGA:
         worst = float(self._hof_fit_host[-1]) if (self.H and self.hof_n >= self.H) else None
         if self.generation < 0:
             inv = (~self.valid).to(torch.uint8)
-            fit = self._evaluate_fused(0, self.population, self._order(inv))
+            fit = self._evaluate_fused(0, self._rows, self._order(inv))
             new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, self.fitness, worst)
             self.fitness, self.valid = new_fit, torch.ones_like(self.valid)
             # generation 1's offspring go to spare[H:] (no swap after the initial
             # update); the initial population is current on every rank
-            self._hof_update_fused(self.population, cand, cand_fit, k, self.spare,
-                                   overlap=lambda: self._next_gen_prep(1, self.population, new_fit, self.spare))
+            self._hof_update_fused(self._rows, cand, cand_fit, k, self.spare,
+                                   overlap=lambda: self._next_gen_prep(1, self._rows, new_fit, self.spare))
             self.store[: self.hof_n] = self.spare[: self.hof_n]
             self.generation = 0
             return self._record(0, nevals, stats)
@@ -672,7 +694,7 @@ class DeviceGA:
         self._mark(None)
         off = self.spare[self.H:]
         if self._next is None or self._next[0] != g:
-            self._next_gen_prep(g, self.population, self.fitness, self.spare)
+            self._next_gen_prep(g, self._rows, self.fitness, self.spare)
         _, inv, inherited, order, sched = self._next
         self._next = None
         self._mark("select_vary")
@@ -686,7 +708,7 @@ class DeviceGA:
             # the side stream (_next_gen_prep), both before generation g + 1's
             # variation overwrites store[H:]
             # (no hall of fame: the candidates are never read)
-            cand_pairs = self._complete(g, off, self.population, cand[:k] if self.H else cand[:0], "cand")
+            cand_pairs = self._complete(g, off, self._rows, cand[:k] if self.H else cand[:0], "cand")
             self._mark("complete", sub=True)
         # generation g + 1's parents are this offspring; its offspring go to
         # store[H:] (this generation's parents, free now), the buffer the swap

@@ -77,6 +77,14 @@ def main(out_dir, mode="small"):
         ga.initialize("normal", 2.0)
         ga.run(3)
         pop = ga.population_full().cpu().numpy()  # (sharded variation: an all-gather of the shards' rows)
+        if ga._sharded():  # a rank holds only its shard current: the plain view refuses
+            try:
+                ga.population
+            except RuntimeError:
+                pass
+            else:
+                raise AssertionError("DeviceGA.population returned rows of a sharded run")
+            assert ga.shard_rows().shape[0] == ga.hi - ga.lo
         if not dist.is_initialized() or dist.get_rank() == 0:
             os.makedirs(out_dir, exist_ok=True)
             np.save(os.path.join(out_dir, "population.npy"), pop)

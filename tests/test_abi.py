@@ -117,6 +117,9 @@ def test_workspace_bytes_follow_the_resolved_kernel(lib):
     a.n_genomes = 3  # fewer genomes than CUs: one block each
     base3 = 256 + (3 * 6 * 4 + 255) // 256 * 256
     assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base3 + (3 * 7 * per_copy + 255) // 256 * 256
+    a.n_games = 8  # more than six games: two work items (chunks of 4) per genome, a block each
+    base38 = 256 + (3 * 8 * 4 + 255) // 256 * 256
+    assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == base38 + (6 * 7 * per_copy + 255) // 256 * 256
 
 
 def test_struct_layout_matches_c(tmp_path):

@@ -363,6 +363,40 @@ def test_horizon_matches_oracle(gpu, oracle, dtype, T):
         assert ref["total_frames"].sum() > n * 6  # multi-episode slots were exercised
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_horizon_long_slots_past_the_serve_table(gpu, oracle, dtype):
+    """A horizon slot carries its point count across auto-resets; at T = 9000
+    most slots pass kServeTabPoints = 64 points, where the serves stop coming
+    from the block's LDS table and come from serve_entry(game_seed, point)
+    (round-4 review: the tabbed slots had kept seed 0 there, so every slot got
+    the same serves).  Bit-exact against the oracle, which serves every point
+    from serve_entry(game_seed, point)."""
+    from pong_amd.device import Evaluator
+    shape = [6, 64, 3]
+    T = 9000
+    rng = np.random.default_rng(5)
+    G = _gene_count(shape)
+    n, H = 64, 16
+    genomes = rng.standard_normal((n, G)) * 3.0
+    opponents = rng.standard_normal((H, G)) * 3.0
+    if dtype == torch.float32:
+        genomes = genomes.astype(np.float32).astype(np.float64)
+        opponents = opponents.astype(np.float32).astype(np.float64)
+    kinds = np.tile(np.array([0, 1, 2, 3, 3, 3], np.int32), (n, 1))
+    opp = rng.integers(0, H, (n, 6)).astype(np.int32)
+    mult = np.where(kinds == 3, 0.5, 1.0)
+    ev = Evaluator(shape, device=gpu, dtype=dtype, horizon=T)
+    res, _ = ev.evaluate(_dev_genomes(genomes, gpu, dtype), torch.tensor(kinds, device=gpu),
+                         torch.tensor(opp, device=gpu), torch.tensor(mult, device=gpu),
+                         opponents=_dev_genomes(opponents, gpu, dtype))
+    torch.cuda.synchronize()
+    ref = oracle.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents, n_threads=8, horizon=T)
+    points = ref["scores"].sum(-1)
+    assert (points > 64).sum() > n, "the regime past the serve table was not exercised"
+    _assert_same(res, ref)
+    assert (res.frames.cpu().numpy() == T).all()
+
+
 def test_horizon_rejected_where_unsupported(gpu):
     from pong_amd import _lib
     from pong_amd.device import Evaluator

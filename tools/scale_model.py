@@ -16,8 +16,12 @@ P = N x 65 536:
     path of a rank's non-evaluation ops at P = N x 65 536 (op by op, sharded
     variation) beyond the same ops at 65 536;
 and prints the projected efficiency (N=1 generation time) / (N generation time)
-with t_N = max-shard eval + replicated(P) + all-gather(P) and t_1 = mean-shard
-eval + replicated(65 536).  The all-gather (fitness f64 + lineage f32 per row)
+with t_N = max-shard eval + replicated(P) + all-gather(P) and t_1 = the MEASURED
+one-GPU generation at 65 536 (the bench's own step: median wall time, round-5
+review), and the same in env-steps/s: (sum of the shards' stepped env-steps /
+t_N) / (N x the one-GPU generation's stepped env-steps / t_1).  Every shard and
+the one-GPU evaluation report their stepped env-steps and ps per env-step, so a
+slower shard is split into more frames vs slower frames.  The all-gather (fitness f64 + lineage f32 per row)
 is priced at 1 TB/s aggregate over xGMI (a conservative reading of 7 x 153
 GB/s links) plus 30 us.
 
@@ -51,7 +55,7 @@ def make_ga(P, dev, seed=1234, sigma=3.0):
 
 
 def timed_steps(ga, steps):
-    """(wall ms, evaluation ms) per generation, steady state."""
+    """(wall ms, evaluation ms, stepped env-steps) per generation, steady state."""
     out = []
     for _ in range(steps):
         ga.eval_events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -60,13 +64,14 @@ def timed_steps(ga, steps):
         ga.step()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) * 1e3
-        out.append((wall, ga.eval_events[0].elapsed_time(ga.eval_events[1])))
+        out.append((wall, ga.eval_events[0].elapsed_time(ga.eval_events[1]), int(ga.last.counters[0].item())))
     ga.eval_events = None
     return out
 
 
 def shard_evals(ga, n_shards):
-    """Each rank's shard of the current population evaluated on its own (ms each)."""
+    """Each rank's shard of the current population evaluated on its own:
+    (ms, stepped env-steps, opponents' record prep ms) each."""
     P, S = ga.P, ga.P // n_shards
     ev = D.Evaluator(ga.nodes, dtype=ga.dtype, device=ga.device, n_games=ga.n_games, seed=ga.ev.seed)
     opponents = ga.hall_of_fame[: ga.hof_n]
@@ -75,14 +80,22 @@ def shard_evals(ga, n_shards):
         lo = r * S
         kind, opp, mult = D.schedule("selfplay", S, ga.n_games, lo, ga.hof_fitness, ga.hof_n, ga.seed,
                                      ga.generation + 1, ga.device)
-        rows = ga.population[lo:lo + S]
+        rows = ga._rows[lo:lo + S]
         ev.evaluate(rows, kind, opp, mult, opponents=opponents, validate=False)  # warm (workspace)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        ev.evaluate(rows, kind, opp, mult, opponents=opponents, validate=False)
+        res, _ = ev.evaluate(rows, kind, opp, mult, opponents=opponents, validate=False)
         b.record()
         torch.cuda.synchronize()
-        ms.append(a.elapsed_time(b))
+        t = a.elapsed_time(b)
+        # the genome records alone (prep="genomes" plays nothing): the rest of the
+        # launch's preparation is the opponents' records (the hall of fame, P/4 rows)
+        c, d = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c.record()
+        ev.evaluate(rows, kind, opp, mult, opponents=opponents, validate=False, prep="genomes")
+        d.record()
+        torch.cuda.synchronize()
+        ms.append((t, int(res.counters[0].item()), c.elapsed_time(d)))
     return ms
 
 
@@ -123,7 +136,7 @@ def replicated_ops(ga, n_shards=1, reps=3):
     timed("select_ranked", lambda: D.select_ranked(fit, P, ga.tournsize, ga.seed, 99, ga.ws, chosen=chosen))
     offspring = ga.spare[ga.H:]
     kw = dict(seed=ga.seed, generation=99, out=offspring)
-    args = (ga.population, chosen, ga.G, ga.cxpb, ga.mutpb, ga.alpha, ga.mu, ga.sigma, ga.indpb)
+    args = (ga._rows, chosen, ga.G, ga.cxpb, ga.mutpb, ga.alpha, ga.mu, ga.sigma, ga.indpb)
     if n_shards == 1:
         timed("vary", lambda: D.vary(*args, **kw))
     else:
@@ -154,7 +167,7 @@ def replicated_ops(ga, n_shards=1, reps=3):
         ch = torch.empty(k, dtype=torch.int64, device=dev)
         pk = torch.empty(old_n + 2 * k, dtype=torch.int64, device=dev)
         timed("hof_prepare", lambda: D.hof_prepare_cand(ga.hof_fitness[:old_n], ga.hof_hash[:old_n], cand[:k],
-                                                       cand_fit[:k], ga.population, ga.G, ch, pk, ga.ws))
+                                                       cand_fit[:k], ga._rows, ga.G, ch, pk, ga.ws))
         pk_h = pk.cpu().numpy()
         n = old_n + k
         t0 = time.perf_counter()
@@ -167,7 +180,7 @@ def replicated_ops(ga, n_shards=1, reps=3):
         hh = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
         hf = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
         dst = torch.empty((m, ga.G), dtype=ga.dtype, device=dev)
-        timed("hof_commit", lambda: D.hof_commit(dst, ga.store, ga.population, cand[:k], src_d, old_n, ga.G,
+        timed("hof_commit", lambda: D.hof_commit(dst, ga.store, ga._rows, cand[:k], src_d, old_n, ga.G,
                                                  ga.hof_hash, ch, hh, nf_d, hf))
     # on the critical path: merge, the candidates' completion (sharded), their
     # prepare and commit; the selection, the parents' completion, the shard's
@@ -192,8 +205,15 @@ def main():
     for _ in range(3):
         ga1.step()
     t1 = timed_steps(ga1, gens)
-    res["p65536_wall_ms"] = [w for w, _ in t1]
-    res["p65536_eval_ms"] = [e for _, e in t1]
+    res["p65536_wall_ms"] = [w for w, _, _ in t1]
+    res["p65536_eval_ms"] = [e for _, e, _ in t1]
+    res["p65536_steps"] = [n for _, _, n in t1]
+    res["p65536_ps_per_step"] = [e * 1e9 / n for _, e, n in t1]
+    sh1 = shard_evals(ga1, 1)
+    res["p65536_own_eval"] = {"ms": sh1[0][0], "steps": sh1[0][1], "genome_prep_ms": sh1[0][2],
+                              "ps_per_step": sh1[0][0] * 1e9 / sh1[0][1]}
+    print(json.dumps({"p65536": {k: res[k] for k in ("p65536_wall_ms", "p65536_eval_ms", "p65536_steps",
+                                                     "p65536_ps_per_step", "p65536_own_eval")}}), flush=True)
     ops1 = replicated_ops(ga1, 1)
     print(json.dumps({"replicated_ops_p65536": ops1}), flush=True)
     res["replicated_ops_p65536"] = ops1
@@ -205,30 +225,43 @@ def main():
         gaN.step()
     walls, evals, shards = [], [], []
     for g in range(gens):
-        (w, e), = timed_steps(gaN, 1)
+        (w, e, _), = timed_steps(gaN, 1)
         walls.append(w)
         evals.append(e)
         sh = shard_evals(gaN, N)
         shards.append(sh)
-        print(json.dumps({"gen": gaN.generation, "wall_ms": w, "eval_ms": e, "shard_ms": sh}), flush=True)
+        print(json.dumps({"gen": gaN.generation, "wall_ms": w, "eval_ms": e, "shard_ms": [x[0] for x in sh],
+                          "shard_steps": [x[1] for x in sh],
+                          "shard_ps_per_step": [x[0] * 1e9 / x[1] for x in sh],
+                          "shard_genome_prep_ms": [x[2] for x in sh]}), flush=True)
     ops = replicated_ops(gaN, N)
     print(json.dumps({"replicated_ops_pN": ops}), flush=True)
     res["replicated_ops_pN"] = ops
-    repl1 = float(np.median([w - e for w, e in t1]))
+    repl1 = float(np.median([w - e for w, e, _ in t1]))
     # a rank at N pays the one-GPU generation's non-evaluation time plus what
     # its P = N x 65 536 ops (sharded variation) cost beyond the same ops at
     # 65 536; its shard-sized work (evaluation prep, order, scatter) as at N = 1
     replN = repl1 + max(0.0, ops["replicated_critical_ms"] - ops1["replicated_critical_ms"])
     res["replicated_ms_pN_wall"] = float(np.median([w - e for w, e in zip(walls, evals)]))
-    shard_max = float(np.median([max(s) for s in shards]))
-    shard_mean = float(np.median([float(np.mean(s)) for s in shards]))
+    shard_max = float(np.median([max(x[0] for x in s) for s in shards]))
+    shard_mean = float(np.median([float(np.mean([x[0] for x in s])) for s in shards]))
+    steps_n = float(np.median([sum(x[1] for x in s) for s in shards]))  # all ranks' stepped env-steps
     allgather = 0.03 + N * S * 12 / 1e12 * 1e3  # ms
     t_n = shard_max + replN + allgather
-    t_1 = shard_mean + repl1
+    t_1 = float(np.median(res["p65536_wall_ms"]))  # the measured one-GPU generation
+    steps_1 = float(np.median(res["p65536_steps"]))
+    ps_1 = float(np.median(res["p65536_ps_per_step"]))
+    ps_n = float(np.median([float(np.mean([x[0] * 1e9 / x[1] for x in s])) for s in shards]))
     res.update({"replicated_ms_p65536": repl1, "replicated_ms_pN": replN, "shard_eval_ms_max": shard_max,
                 "shard_eval_ms_mean": shard_mean, "straggler_factor": shard_max / shard_mean,
+                "one_gpu_eval_ms": float(np.median(res["p65536_eval_ms"])),
+                "steps_per_shard_pN": steps_n / N, "steps_one_gpu": steps_1,
+                "ps_per_step_shard_pN": ps_n, "ps_per_step_one_gpu": ps_1,
                 "allgather_ms_model": allgather, "t1_ms": t_1, "tN_ms": t_n, "projected_efficiency": t_1 / t_n,
-                "projected_speedup": N * t_1 / t_n})
+                "projected_speedup": N * t_1 / t_n,
+                "projected_env_steps_per_s_N": steps_n / (t_n / 1e3),
+                "env_steps_per_s_1": steps_1 / (t_1 / 1e3),
+                "projected_efficiency_env_steps": (steps_n / t_n) / (N * steps_1 / t_1)})
     print(json.dumps(res), flush=True)
 
 
