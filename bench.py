@@ -47,7 +47,7 @@ import torch.distributed as dist  # noqa: E402
 
 F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
-PROFILE_ROUND = "r04"           # profiles/<round>/ holds the PMC passes of the committed build
+PROFILE_ROUND = "r05"           # profiles/<round>/ holds the PMC passes of the committed build
 
 
 def parse():
@@ -135,8 +135,12 @@ def main():
     # the device-resident eaSimple (pong_amd.evolve): replicated population,
     # rank r evaluates its shard, one all-gather of fitness per generation;
     # GA parameters are config.py's (cxpb = mutpb = indpb = alpha = sigma = 0.9, mu = 0)
+    # self-play: each GPU's block of n_local genomes plays its interleaved 1/N slice
+    # of the hall (pg_schedule_args.hof_slices) -- the per-GPU work,
+    # opponents included, stays that of N = 1 (K = 1 there: the plain schedule)
     ga = DeviceGA(shape, P, H, tournsize, dtype=dtype, device=dev, n_games=args.games, schedule=args.schedule,
-                  seed=args.seed, kernel=args.kernel)
+                  seed=args.seed, kernel=args.kernel,
+                  hof_block_rows=n_local if (args.config == "selfplay" and args.schedule == "selfplay") else 0)
     ga.ev.group_lanes = args.group_lanes
     ga.ev.horizon = args.horizon  # pg_eval_args.horizon: 0 = evaluate()'s episodes
     ga.order_by_length = os.environ.get("PG_NO_LENGTH_ORDER") != "1"  # A/B switch for the evaluation order
@@ -302,10 +306,15 @@ def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_pe
     HBM traffic from the committed PMC passes of the same build and command."""
     wt = 8 if dtype == torch.float64 else 4
     pmc, src = _pmc(_pmc_name(args))
-    traffic = pmc.get("traffic_bytes") if pmc else None
+    # MI355X_MICROARCH.md (HBM / rocprofv3): on gfx950 FETCH_SIZE counts half the
+    # bytes of 16-B-per-lane reads -- the width of every k_service global load
+    # (load_rec's float4 pieces of the lane records) -- so traffic = 2 x FETCH_SIZE
+    # + WRITE_SIZE; the uncorrected sum is reported beside it
+    traffic = pmc.get("traffic_bytes_fetch_x2") if pmc else None
+    traffic_raw = pmc.get("traffic_bytes") if pmc else None
     stale = _pmc_stale(pmc)
     if stale:  # counters of another build: not this kernel's traffic
-        traffic = None
+        traffic = traffic_raw = None
     unique = (n_local + H) * G * wt  # every genome row and hall-of-fame row once
     kernel_s = kernel_ms_mean / 1e3
     return {"bound": "valu", "achieved": achieved_tflops, "peak": F32_VECTOR_PEAK_TFLOPS,
@@ -316,15 +325,18 @@ def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_pe
             "unique_row_bytes_per_launch": unique,
             "refetch_ratio": traffic / unique if traffic else None,
             "traffic_stale": stale,
+            "traffic_uncorrected": traffic_raw,
             "traffic_note": "HBM-side bytes per launch (L2 memory-side requests, MALL hits included): rocprofv3 "
-                            "FETCH_SIZE + WRITE_SIZE of the same bench command, separate --pmc passes (%s); each "
-                            "game loads both networks, so genome rows are fetched ~refetch_ratio times; hbm_GBps = "
-                            "traffic / this run's kernel time" % src,
+                            "2 x FETCH_SIZE + WRITE_SIZE of the same bench command, separate --pmc passes (%s); "
+                            "FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 rule for 16-B-per-lane reads "
+                            "(traffic_uncorrected = FETCH_SIZE + WRITE_SIZE); each game loads both networks' lane "
+                            "records, so genome rows are fetched ~refetch_ratio times; hbm_GBps = traffic / this "
+                            "run's kernel time" % src,
             "engine": "compute-bound on the f32 vector ALU (v_pk_fma_f32, v_exp_f32, v_rcp_f32), no MFMA: every "
                       "game has its own 64x7 and 3x64 matrices applied to one input column; peak = MI355X f32 dense "
                       "peak (157.3 TF, equal for VALU and MFMA); the kernel is VALU-issue-bound: most VALU "
                       "instructions per env-step are physics, features, certificate and bookkeeping, not the "
-                      "network's FMAs (DESIGN.md 4.1, profiles/%s/pmc_sq_k_service.txt)" % PROFILE_ROUND,
+                      "network's FMAs (DESIGN.md 4.1; SQ counters: profiles/%s/sq_summary_final.txt)" % PROFILE_ROUND,
             "kernel": "k_service<8,16,3,double> (pg_eval_population: 8 games per wave, 4 lanes per network, "
                       "f64 service wave per block)",
             "kernel_ms_per_launch": kernel_ms_mean,

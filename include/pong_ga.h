@@ -294,6 +294,14 @@ typedef struct pg_ga_args {
    * first and, once the fitness all-gather has named them, the hall-of-fame
    * candidates and the next selection's parents. */
   const uint8_t *pair_mask;
+  /* ABI 10: or a compact list of the pairs to vary -- pair_list[0 .. *pair_count)
+   * (device; pair_cap >= *pair_count bounds the launch) -- so a completion that
+   * varies a few thousand of P / 2 pairs launches that many waves, not one per
+   * pair.  Only the listed pairs' rows and invalid flags are written (pair_mask
+   * is then ignored); pg_ga_list_pairs turns a mask into such a list. */
+  const int32_t *pair_list;
+  const int32_t *pair_count;
+  int32_t pair_cap;
 } pg_ga_args;
 
 typedef struct pg_select_args {
@@ -316,6 +324,14 @@ typedef enum pg_schedule_mode {
   /* every game against hall-of-fame row ((row_offset + i) * n_games + g) mod n_hof */
   PG_SCHED_SELFPLAY = 1
 } pg_schedule_mode;
+/* PG_SCHED_SELFPLAY with hof_slices K > 1 (ABI 10): the hall is K interleaved
+ * slices (slice b = members b, b + K, b + 2K, ... of [0, n_hof)), and the
+ * genomes of global row block b' = row / block_rows play slice b = b' mod K:
+ * game g of row r against slice member ((r * n_games + g) mod |slice b|), i.e.
+ * hall row that * K + b (slice_local: the index within the slice, for a caller
+ * that passes the slice itself as the opponents -- a rank whose shard is one
+ * block needs only its slice's lane records).  Every slice spans
+ * the whole fitness order, so the blocks face statistically equal opponents. */
 
 typedef struct pg_schedule_args {
   int32_t mode;                  /* pg_schedule_mode */
@@ -330,6 +346,9 @@ typedef struct pg_schedule_args {
   int32_t *opp;                  /* out [n, n_games] device */
   double *mult;                  /* out [n, n_games] device */
   const int32_t *rows;           /* optional [n] device: global row of entry i (NULL: row_offset + i) */
+  int32_t hof_slices;            /* ABI 10, PG_SCHED_SELFPLAY: K slices of the hall (0 or 1: one, as before) */
+  int32_t block_rows;            /* rows per genome block (K > 1: >= 1) */
+  int32_t slice_local;           /* 1: opp = index within the block's slice; 0: hall row */
 } pg_schedule_args;
 
 /* HallOfFame.update (DEAP) over host arrays.  Members are in HallOfFame.items
@@ -438,6 +457,9 @@ int32_t pg_ga_vary(const pg_ga_args *args, void *stream);
  * rows outside [0, 2 n_pairs) are skipped). */
 int32_t pg_ga_mark_pairs(uint8_t *pair_mask, int32_t n_pairs, const int32_t *rows, int32_t n_rows,
                          int32_t skip_lo, int32_t skip_hi, const uint8_t *exclude, void *stream);
+/* list[0 .. *count) = the pairs j with pair_mask[j] != 0, in no particular order
+ * (*count set by the call; list [n_pairs] or at least as long as the marks). */
+int32_t pg_ga_list_pairs(const uint8_t *pair_mask, int32_t n_pairs, int32_t *list, int32_t *count, void *stream);
 int32_t pg_ga_schedule(const pg_schedule_args *args, void *stream);
 /* hash[i] = 64-bit hash of the genes of row index[i] (row i if index is NULL):
  * f32/f64 bit patterns, -0.0 as 0.0, so equal gene lists hash equal. */

@@ -521,12 +521,12 @@ __device__ __forceinline__ int group_broadcast(int v, int leader_lane) {
 // ================================================ split-lane helpers ==
 template <int L>
 __device__ __forceinline__ int other_half(int v) {
-  // (every lane reads a valid source lane, so the old value is never kept: no
-  // v_mov of a zero ahead of the DPP move)
+  // (every lane reads a valid source lane, so no old value is needed: one
+  // v_mov_b32_dpp, no copy or zero ahead of it)
   if constexpr (L == 8) {
-    return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);  // row_half_mirror: i <-> 7-i
+    return __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror: i <-> 7-i
   } else if constexpr (L == 16) {
-    return __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);  // row_mirror: i <-> 15-i
+    return __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);  // row_mirror: i <-> 15-i
   } else if constexpr (L == 32) {
     const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
     return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];

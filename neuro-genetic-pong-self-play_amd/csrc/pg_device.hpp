@@ -96,6 +96,10 @@ struct Pong {
     static_assert(kPaddleSpeed == 3, "the table below");
     return clamp_row(y + __builtin_amdgcn_sbfe(0x0003FD00, 8 * code, 8));
   }
+  // the same for a code kept as 8 x code (the table's bit offset: k_service)
+  __device__ static int move_player8(int y, int code8) {
+    return clamp_row(y + __builtin_amdgcn_sbfe(0x0003FD00, code8, 8));
+  }
 
   // env.step(action) (main.py:77): right [up,down] = action[4:6], left = action[6:8].
   // The common case -- the ball in flight, away from both paddle faces -- is
@@ -117,12 +121,17 @@ struct Pong {
   // 1-player env (k_service keeps it from its game starts: no test per frame)
   template <class ServeOf>
   __device__ int step(int right_code, int left_code, ServeOf serve_of, bool any_one_player) {
+    return step_c<false>(right_code, left_code, serve_of, any_one_player);
+  }
+  // kC8: the codes come as 8 x code (k_service keeps its actions so)
+  template <bool kC8, class ServeOf>
+  __device__ int step_c(int right_code, int left_code, ServeOf serve_of, bool any_one_player) {
     int ev = kStepFly;
-    rpy = move_player(rpy, right_code);
+    rpy = kC8 ? move_player8(rpy, right_code) : move_player(rpy, right_code);
     // left paddle: the action, or the built-in CPU of the 1-player env
     // (main.py:40) -- behind a wave-uniform test: no game of a self-play
     // schedule takes it
-    int nl = move_player(lpy, left_code);
+    int nl = kC8 ? move_player8(lpy, left_code) : move_player(lpy, left_code);
     if (__builtin_expect(any_one_player, 0)) {
       const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
       const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
@@ -278,16 +287,23 @@ __device__ inline int paddle_c2(int py) {
 __device__ inline int clamp_action(int c2, int code) {
   return c2 < 32 ? 2 : (c2 > 2 * (kFieldH - 16) ? 1 : code);
 }
+__device__ inline int clamp_action8(int c2, int code8) {  // the same on 8 x code
+  return c2 < 32 ? 16 : (c2 > 2 * (kFieldH - 16) ? 8 : code8);
+}
 
 // HardcodedAi.run (dumb_ais.py:2-8) on inference() features: compares
 // ball_y/160 (x[1]) with me/160 (x[4]); the /160 is monotone, so the doubled
 // integer centroids compare the same way.
 __device__ inline int hardcoded(int by2, int me2) { return by2 < me2 ? 1 : (by2 > me2 ? 2 : 0); }
+__device__ inline int hardcoded8(int by2, int me2) { return by2 < me2 ? 8 : (by2 > me2 ? 16 : 0); }
 
 // argmax index -> action code (numpy_nn.py:131-137; index >= 2 -> no-op, the
 // build's extension for 3-output networks).
 __device__ inline int index_to_code(int idx) {  // 0 -> 1, 1 -> 2, 2, 3 -> 0: bits 2 idx of 0b1001
   return (int)__builtin_amdgcn_ubfe(9u, 2u * (unsigned)idx, 2u);
+}
+__device__ inline int index_to_code8(int idx) {  // 8 x index_to_code: byte idx of 0x1008
+  return (int)__builtin_amdgcn_ubfe(0x1008u, 8u * (unsigned)idx, 8u);
 }
 
 // ---- wave-level helpers ----

@@ -231,6 +231,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   // no-score counter (main.py:128-135) = sframe - (tend - TIMEOUT_THRESH), so a
   // plain frame updates neither; total (main.py:73) and the score-based end
   // (main.py:102-107) change only at a point, inside the rare block
+  // act_r / act_l: the actions written into action[4:6] / [6:8] (main.py:91-92)
+  // as 8 x code (code 0 = [0,0], 1 = up, 2 = down), the next step's table offset
   int kind = 0, act_r = 0, act_l = 0, total = 0, fstart = 0, tend = 0, c_vis = 0, tab_off = 0;
   int sframe = 0;
   const WT *gm = genomes;
@@ -335,8 +337,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         st.rpy = Pong::drift(st.rpy, h);
         if (!st.one_player) st.lpy = Pong::drift(st.lpy, h);
         st.timer = 1;
-        act_r = clamp_action(paddle_c2(st.rpy), 0);
-        act_l = clamp_action(paddle_c2(st.lpy), 0);
+        act_r = clamp_action8(paddle_c2(st.rpy), 0);
+        act_l = clamp_action8(paddle_c2(st.lpy), 0);
         fstart -= h;  // frames += h, and the no-score counter with them
         tend -= h;
         hidden += h;
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifdef PG_PATH_PROBE
     const int pt_b = st.point, hits_b = st.hits;
 #endif
-    const int ev = st.step(act_r, act_l, [&](int pt) {
+    const int ev = st.template step_c<true>(act_r, act_l, [&](int pt) {
       return tabbed && pt < kServeTabPoints ? serve_tab[tab_off + pt] : Pong::serve_entry(st.seed, pt);
     }, w_onep);
     const bool bounced = ev == kStepBounce;  // a paddle returned the ball this frame
@@ -435,25 +437,25 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         }
       }
       }
-      const int mine = index_to_code(idx);
+      const int mine = index_to_code8(idx);
       const int other = other_half<L>(mine);
       right = side ? other : mine;
       left = side ? mine : other;
       // HardcodedAi / ScoreHardcodedAi (dumb_ais.py): behind a wave-uniform
       // test, which a self-play schedule never passes
       if (__builtin_expect(w_scripted, 0) && !left_nn) {
-        left = hardcoded(by2, lc2);
+        left = hardcoded8(by2, lc2);
         if (kind == kOppScore && st.s1 > st.s2) left = 0;
       }
       c_vis += 1;  // forwards: c_vis x (1 or 2 networks), counted at the game's end
     }
-    act_l = clamp_action(lc2, left);
-    act_r = clamp_action(rc2, right);
+    act_l = clamp_action8(lc2, left);
+    act_r = clamp_action8(rc2, right);
 #ifndef PG_TIMELINE
     if (!kUntraced && p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
       const int frames = sframe - fstart;
       if (w < p.trace_games && frames <= p.trace_cap && lig == 0)
-        p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(act_r | (act_l << 2) | (vis << 4));
+        p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)((act_r >> 3) | ((act_l >> 3) << 2) | (vis << 4));
     }
 #endif
     // calculate_timeout_and_frames (main.py:128-135); at most one point a frame
@@ -498,7 +500,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     const int timeout = sframe - (tend - kTimeoutThresh);
     if (rally_check && timeout <= kTimeoutThresh) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
-      const uint64_t key = rally_key(st, act_r, act_l);
+      const uint64_t key = rally_key(st, act_r >> 3, act_l >> 3);
       const int at = slots[rs].rally_at;
       if (at > timeout || at < 0) {
         if (lig == 0) {

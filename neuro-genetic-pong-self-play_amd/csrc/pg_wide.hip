@@ -860,11 +860,14 @@ bool wide_shape_ok(const pg_net &n, int n_games) {
          n_games >= 1 && n_games <= 64;
 }
 
-// games per work item (k_wide's NG): 6, so GAMES_TO_PLAY = 6 plays a genome's
-// games in one lockstep pass; more games are split into balanced chunks
-// (k_wide<8> spilled 112 VGPRs: round-4 review)
-constexpr int kWideNG = 6;
-static int wide_items(int n_genomes, int n_games) { return n_genomes * ((n_games + kWideNG - 1) / kWideNG); }
+// games per work item (k_wide's NG): with f32 genes 6, so GAMES_TO_PLAY = 6
+// plays a genome's games in one lockstep pass; more games are split into
+// balanced chunks (k_wide<8> spilled 112 VGPRs: round-4 review).  With f64
+// genes 4: k_wide<6, double> spilled 25 VGPRs (its wider tail pieces), so a
+// 6-game genome is two items of 3 -- the genome's W2 streamed twice per frame
+// on the f64-storage path (config 5 and the bench store f32 genes).
+static int wide_ng(int dtype) { return dtype == PG_F64 ? 4 : 6; }
+static int wide_items(int n_genomes, int n_games, int ng) { return n_genomes * ((n_games + ng - 1) / ng); }
 
 static int wide_grid(int n_items) {
   const int cap = num_cus();
@@ -873,10 +876,10 @@ static int wide_grid(int n_items) {
 
 size_t wide_workspace_bytes(const pg_eval_args *a) {
   if (!a || a->n_genomes <= 0 || a->net.n_nodes != 4) return 0;
-  const int NG = kWideNG;
+  const int NG = wide_ng(a->net.dtype);
   const WideLayout l = wide_layout(a->net.nodes[1], a->net.nodes[2], a->net.bias ? 1 : 0,
                                    a->net.dtype == PG_F64 ? 8 : 4);
-  return (size_t)wide_grid(wide_items(a->n_genomes, a->n_games)) * (size_t)(NG + 1) * (size_t)l.net_bytes;
+  return (size_t)wide_grid(wide_items(a->n_genomes, a->n_games, NG)) * (size_t)(NG + 1) * (size_t)l.net_bytes;
 }
 
 template <int NG, typename WT>
@@ -890,7 +893,7 @@ static int32_t launch_wide_t(EvalParams p, void *scratch, hipStream_t s) {
   // above 64 KB of dynamic LDS; an older runtime that rejects the attribute launches anyway
   (void)hipFuncSetAttribute((const void *)k_wide<NG, WT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   (void)hipGetLastError();
-  const int grid = wide_grid(wide_items(p.n_genomes, p.n_games));  // wide_workspace_bytes sized the scratch for it
+  const int grid = wide_grid(wide_items(p.n_genomes, p.n_games, NG));  // wide_workspace_bytes sized the scratch for it
   if (grid <= 0) return PG_OK;
   p.wide_scratch = scratch;
   hipLaunchKernelGGL((k_wide<NG, WT>), dim3(grid), dim3(kWideThreads), (size_t)lds, s, p);
@@ -899,8 +902,7 @@ static int32_t launch_wide_t(EvalParams p, void *scratch, hipStream_t s) {
 }
 
 int32_t launch_wide(const EvalParams &p, int dtype, void *scratch, hipStream_t s) {
-  return dtype == PG_F64 ? launch_wide_t<kWideNG, double>(p, scratch, s)
-                         : launch_wide_t<kWideNG, float>(p, scratch, s);
+  return dtype == PG_F64 ? launch_wide_t<4, double>(p, scratch, s) : launch_wide_t<6, float>(p, scratch, s);
 }
 
 }  // namespace pg

@@ -473,7 +473,11 @@ __device__ __forceinline__ double rng_u01(uint64_t key, uint64_t b) {
 template <typename WT>
 __global__ __launch_bounds__(256) void k_vary(pg_ga_args a) {
   const int pairs = (a.n + 1) / 2;
-  const int pair = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  int pair = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (a.pair_list) {  // a compact list of the pairs to write (pong_ga.h)
+    if (pair >= __builtin_amdgcn_readfirstlane(*a.pair_count)) return;
+    pair = __builtin_amdgcn_readfirstlane(a.pair_list[pair]);
+  }
   if (pair >= pairs) return;
   const int lane = threadIdx.x & 63;
   const int i0 = 2 * pair, i1 = 2 * pair + 1;
@@ -485,7 +489,7 @@ __global__ __launch_bounds__(256) void k_vary(pg_ga_args a) {
     a.invalid[i0] = (uint8_t)(cx || mut0);
     if (has1) a.invalid[i1] = (uint8_t)(cx || mut1);
   }
-  if (a.pair_mask && !a.pair_mask[pair]) return;  // a pair this call does not write (pong_ga.h)
+  if (!a.pair_list && a.pair_mask && !a.pair_mask[pair]) return;  // a pair this call does not write (pong_ga.h)
   const uint64_t k3 = rng_key(a.seed, a.generation, 3, (uint64_t)pair);
   const uint64_t k5 = rng_key(a.seed, a.generation, 5, (uint64_t)pair);
   const uint64_t k6 = rng_key(a.seed, a.generation, 6, (uint64_t)pair);
@@ -556,6 +560,12 @@ __global__ void k_mark_pairs(uint8_t *mask, int n_pairs, const int32_t *rows, in
   if ((j < skip_lo || j >= skip_hi) && !(exclude && exclude[j])) mask[j] = 1;
 }
 
+// pg_ga_list_pairs: the marked pairs appended to a list (order irrelevant).
+__global__ void k_list_pairs(const uint8_t *mask, int n_pairs, int32_t *list, int32_t *count) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n_pairs && mask[j]) list[atomicAdd(count, 1)] = j;
+}
+
 // Opponent schedule of evaluate() (main.py:28-66) for rows [0, n).
 __global__ void k_schedule(pg_schedule_args a) {
   const long w = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -568,7 +578,15 @@ __global__ void k_schedule(pg_schedule_args a) {
   if (a.mode == PG_SCHED_SELFPLAY) {
     if (a.n_hof > 0) {
       kind = kOppNN;
-      opp = (int)((row * a.n_games + g) % a.n_hof);
+      const int K = a.hof_slices > 1 && a.n_hof >= a.hof_slices ? a.hof_slices : 1;
+      if (K == 1) {
+        opp = (int)((row * a.n_games + g) % a.n_hof);
+      } else {  // the block's interleaved slice of the hall (pong_ga.h)
+        const int b = (int)((row / a.block_rows) % K);
+        const long m = (a.n_hof - b + K - 1) / K;
+        const int k = (int)((row * a.n_games + g) % m);
+        opp = a.slice_local ? k : k * K + b;
+      }
     }
   } else if (g < 3) {
     kind = g == 0 ? kOppHard : (g == 1 ? kOppRomCpu : kOppScore);
@@ -1139,11 +1157,24 @@ int32_t pg_ga_vary(const pg_ga_args *a, void *stream) {
     return fail(PG_ERR_INVALID, "varAnd: bad sizes or NULL buffers");
   if (a->n == 0) return PG_OK;
   const int pairs = (a->n + 1) / 2;
-  const dim3 grid((unsigned)((pairs + 3) / 4));  // one wave per pair
+  if (a->pair_list && (!a->pair_count || a->pair_cap < 0)) return fail(PG_ERR_INVALID, "varAnd: pair_list needs pair_count and pair_cap >= 0");
+  const int waves = a->pair_list ? (a->pair_cap < pairs ? a->pair_cap : pairs) : pairs;
+  if (waves == 0) return PG_OK;
+  const dim3 grid((unsigned)((waves + 3) / 4));  // one wave per pair
   if (a->dtype == PG_F64)
     hipLaunchKernelGGL(k_vary<double>, grid, dim3(256), 0, (hipStream_t)stream, *a);
   else
     hipLaunchKernelGGL(k_vary<float>, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  PG_HIP(hipGetLastError());
+  return PG_OK;
+}
+
+int32_t pg_ga_list_pairs(const uint8_t *mask, int32_t n_pairs, int32_t *list, int32_t *count, void *stream) {
+  if (n_pairs < 0 || !count || (n_pairs && (!mask || !list))) return fail(PG_ERR_INVALID, "list_pairs: bad sizes or NULL buffers");
+  PG_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), (hipStream_t)stream));
+  if (n_pairs == 0) return PG_OK;
+  hipLaunchKernelGGL(k_list_pairs, dim3((unsigned)((n_pairs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mask,
+                     n_pairs, list, count);
   PG_HIP(hipGetLastError());
   return PG_OK;
 }
@@ -1168,6 +1199,7 @@ int32_t pg_ga_schedule(const pg_schedule_args *a, void *stream) {
   if (!a->kind || !a->opp || !a->mult || (a->mode == PG_SCHED_REFERENCE && a->n_hof > 0 && !a->hof_fitness))
     return fail(PG_ERR_INVALID, "schedule: NULL output or hof_fitness");
   const long total = (long)a->n * a->n_games;
+  if (a->hof_slices > 1 && a->block_rows < 1) return fail(PG_ERR_INVALID, "schedule: hof_slices > 1 needs block_rows >= 1");
   hipLaunchKernelGGL(k_schedule, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *a);
   PG_HIP(hipGetLastError());
   return PG_OK;

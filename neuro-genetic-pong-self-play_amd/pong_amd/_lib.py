@@ -95,6 +95,7 @@ class PgGaArgs(ctypes.Structure):
         ("cxpb", ctypes.c_double), ("mutpb", ctypes.c_double), ("alpha", ctypes.c_double),
         ("mu", ctypes.c_double), ("sigma", ctypes.c_double), ("indpb", ctypes.c_double),
         ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64), ("pair_mask", _vp),
+        ("pair_list", _vp), ("pair_count", _vp), ("pair_cap", ctypes.c_int32),
     ]
 
 
@@ -111,6 +112,7 @@ class PgScheduleArgs(ctypes.Structure):
         ("row_offset", ctypes.c_int64), ("n_hof", ctypes.c_int32), ("hof_fitness", _vp),
         ("seed", ctypes.c_uint64), ("generation", ctypes.c_uint64),
         ("kind", _vp), ("opp", _vp), ("mult", _vp), ("rows", _vp),
+        ("hof_slices", ctypes.c_int32), ("block_rows", ctypes.c_int32), ("slice_local", ctypes.c_int32),
     ]
 
 
@@ -192,6 +194,7 @@ SIGNATURES = {
     "pg_ga_select_tournament": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp]),
     "pg_ga_select_tournament_ranked": (ctypes.c_int32, [ctypes.POINTER(PgSelectArgs), _vp, _vp, _vp]),
     "pg_ga_vary": (ctypes.c_int32, [ctypes.POINTER(PgGaArgs), _vp]),
+    "pg_ga_list_pairs": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp, _vp]),
     "pg_ga_mark_pairs": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                           _vp, _vp]),
     "pg_ga_schedule": (ctypes.c_int32, [ctypes.POINTER(PgScheduleArgs), _vp]),

@@ -35,7 +35,8 @@ FORMAT = "pong_amd.device_ga/1"
 _DT = {torch.float64: "F64", torch.float32: "F32", torch.int64: "I64", torch.int32: "I32", torch.uint8: "U8"}
 _TD = {v: k for k, v in _DT.items()}
 _CONFIG_KEYS = ("nodes", "population_size", "hof_size", "tournsize", "bias", "dtype", "n_games", "schedule",
-                "cxpb", "mutpb", "alpha", "mu", "sigma", "indpb", "seed", "physics_seed", "precision", "kernel")
+                "cxpb", "mutpb", "alpha", "mu", "sigma", "indpb", "seed", "physics_seed", "precision", "kernel",
+                "hof_block_rows")
 
 
 def write_tensors(path: str, tensors: dict, metadata: dict, block_bytes: int = 1 << 28) -> None:
@@ -91,7 +92,7 @@ def _config(ga) -> dict:
             "bias": ga.bias, "dtype": str(ga.dtype).replace("torch.", ""), "n_games": ga.n_games,
             "schedule": ga.schedule, "cxpb": ga.cxpb, "mutpb": ga.mutpb, "alpha": ga.alpha, "mu": ga.mu,
             "sigma": ga.sigma, "indpb": ga.indpb, "seed": ga.seed, "physics_seed": ga.physics_seed,
-            "precision": ga.precision, "kernel": ga.kernel}
+            "precision": ga.precision, "kernel": ga.kernel, "hof_block_rows": ga.hof_block_rows}
 
 
 def save(ga, path: str) -> str:

@@ -46,6 +46,17 @@ def _need(t: torch.Tensor, name: str, dtype, device, shape=None):
         raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
 
 
+def _need_rows(t: torch.Tensor, name: str, dtype, device):
+    """A row-major matrix whose rows may be strided (pg_eval_args.opponent_stride):
+    e.g. a rank's slice hall[b::K] of the hall of fame."""
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name} must live on {device}, got {t.device}")
+    if t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1) or (t.shape[0] > 1 and t.stride(0) < t.shape[1]):
+        raise ValueError(f"{name} must be row-major rows (unit column stride, row stride >= row length)")
+
+
 @dataclass
 class EvalResult:
     """evaluate() outputs for a batch, all on the device."""
@@ -143,7 +154,7 @@ class Evaluator:
         _need(opp, "opp", torch.int32, dev, (n, games))
         _need(mult, "mult", torch.float64, dev, (n, games))
         if opponents is not None:
-            _need(opponents, "opponents", self.dtype, dev)
+            _need_rows(opponents, "opponents", self.dtype, dev)
             if opponents.dim() != 2 or opponents.shape[1] < self.genes:
                 raise ValueError(f"opponents must be [H, >= {self.genes}], got {tuple(opponents.shape)}")
         if rows is not None:
@@ -373,7 +384,8 @@ def select_tournament_ranked(fitness: torch.Tensor, k: int, tournsize: int, seed
 
 def vary(parents: torch.Tensor, chosen: torch.Tensor, genes: int, cxpb: float, mutpb: float, alpha: float,
          mu: float, sigma: float, indpb: float, seed: int, generation: int, out: Optional[torch.Tensor] = None,
-         pair_mask: Optional[torch.Tensor] = None, invalid: Optional[torch.Tensor] = None):
+         pair_mask: Optional[torch.Tensor] = None, invalid: Optional[torch.Tensor] = None,
+         pair_list: Optional[tuple] = None):
     """algorithms.varAnd(cxBlend, mutGaussian) on device: returns (offspring, invalid[n] uint8).
     ``pair_mask`` ([(n + 1) // 2] uint8): only the marked pairs' rows are
     written (the invalid flags of every row are); see pg_ga_args.pair_mask."""
@@ -394,11 +406,29 @@ def vary(parents: torch.Tensor, chosen: torch.Tensor, genes: int, cxpb: float, m
     a.cxpb, a.mutpb, a.alpha, a.mu, a.sigma, a.indpb = cxpb, mutpb, alpha, mu, sigma, indpb
     a.seed, a.generation = seed, generation
     a.pair_mask = _ptr(pair_mask)
+    if pair_list is not None:  # (list [cap] int32, count [1] int32, cap): only the listed pairs
+        lst, cnt, cap = pair_list
+        _need(lst, "pair_list", torch.int32, dev)
+        _need(cnt, "pair_count", torch.int32, dev, (1,))
+        a.pair_list, a.pair_count, a.pair_cap = _ptr(lst), _ptr(cnt), int(min(cap, lst.numel()))
     if out.stride(0) != parents.stride(0):
         raise ValueError("offspring and parents must share the row stride")
     with torch.cuda.device(dev):
         L.check("pg_ga_vary", L.lib().pg_ga_vary(ctypes.byref(a), _stream(dev)))
     return out, invalid
+
+
+def list_pairs(mask: torch.Tensor, out: torch.Tensor, count: torch.Tensor) -> None:
+    """pg_ga_list_pairs: out[:count] = the marked pairs (any order)."""
+    dev = mask.device
+    _need(mask, "pair_mask", torch.uint8, dev)
+    _need(out, "pair_list", torch.int32, dev)
+    _need(count, "pair_count", torch.int32, dev, (1,))
+    if out.numel() < mask.numel():
+        raise ValueError("pair_list must hold every pair")
+    with torch.cuda.device(dev):
+        L.check("pg_ga_list_pairs", L.lib().pg_ga_list_pairs(_ptr(mask), mask.numel(), _ptr(out), _ptr(count),
+                                                             _stream(dev)))
 
 
 def mark_pairs(mask: torch.Tensor, rows: torch.Tensor, skip: tuple = (0, 0),
@@ -419,9 +449,13 @@ SCHEDULES = {"reference": L.PG_SCHED_REFERENCE, "selfplay": L.PG_SCHED_SELFPLAY}
 
 
 def schedule(mode: str, n: int, n_games: int, row_offset: int, hof_fitness: Optional[torch.Tensor], n_hof: int,
-             seed: int, generation: int, device, rows: Optional[torch.Tensor] = None):
+             seed: int, generation: int, device, rows: Optional[torch.Tensor] = None, hof_slices: int = 1,
+             block_rows: int = 0, slice_local: bool = False):
     """pg_ga_schedule: (kind, opp, mult) [n, n_games] of evaluate()'s games on device;
-    ``rows`` ([n] int32) gives entry i's global population row (default row_offset + i)."""
+    ``rows`` ([n] int32) gives entry i's global population row (default row_offset + i).
+    Self-play with ``hof_slices`` K > 1: the genomes of row block r // block_rows
+    play the hall's interleaved slice (r // block_rows) mod K (pong_ga.h); with
+    ``slice_local`` opp indexes the slice (pass ``hall[b::K]`` as the opponents)."""
     dev = torch.device(device)
     kind = torch.empty((n, n_games), dtype=torch.int32, device=dev)
     opp = torch.empty((n, n_games), dtype=torch.int32, device=dev)
@@ -435,7 +469,8 @@ def schedule(mode: str, n: int, n_games: int, row_offset: int, hof_fitness: Opti
     if rows is not None:
         _need(rows, "rows", torch.int32, dev, (n,))
     a = L.PgScheduleArgs(SCHEDULES[mode], n, n_games, row_offset, n_hof, _ptr(hof_fitness), seed, generation,
-                         _ptr(kind), _ptr(opp), _ptr(mult), _ptr(rows))
+                         _ptr(kind), _ptr(opp), _ptr(mult), _ptr(rows), int(hof_slices), int(block_rows),
+                         1 if slice_local else 0)
     with torch.cuda.device(dev):
         L.check("pg_ga_schedule", L.lib().pg_ga_schedule(ctypes.byref(a), _stream(dev)))
     return kind, opp, mult

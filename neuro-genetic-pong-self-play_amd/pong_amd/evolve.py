@@ -58,7 +58,7 @@ class DeviceGA:
                  n_games: int = 6, schedule: str = "reference", cxpb: float = 0.9, mutpb: float = 0.9,
                  alpha: float = 0.9, mu: float = 0.0, sigma: float = 0.9, indpb: float = 0.9,
                  seed: int = 0, physics_seed: int = 0, precision: str = "certified", kernel: str = "auto",
-                 group=None):
+                 group=None, hof_block_rows: int = 0):
         if schedule not in D.SCHEDULES:
             raise ValueError(f"schedule must be one of {sorted(D.SCHEDULES)}")
         self.nodes = [int(v) for v in nodes]
@@ -80,6 +80,19 @@ class DeviceGA:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.lo, self.hi = PD.shard_range(self.P, self.rank, self.world)
+        # Self-play against a sliced hall (pg_schedule_args.hof_slices):
+        # with hof_block_rows B > 0 the genomes of row block r // B play the hall's
+        # interleaved slice (r // B) mod K, K = ceil(P / B) -- a function of the
+        # global row, so any sharding plays the same games; a rank whose shard is
+        # one block passes only its slice (1/K of the hall's lane records).  P <= B:
+        # K = 1, the plain schedule.
+        self.hof_block_rows = int(hof_block_rows)
+        self.hof_slices = 1
+        if self.hof_block_rows > 0 and schedule == "selfplay":
+            self.hof_slices = max(1, min(-(-self.P // self.hof_block_rows), max(self.H, 1)))
+        B = self.hof_block_rows
+        self._slice = (self.lo // B if self.hof_slices > 1 and self.hi > self.lo and self.lo // B == (self.hi - 1) // B
+                       else None)
         self.store = torch.zeros((self.H + self.P, self.G), dtype=dtype, device=self.device)
         self.spare = torch.empty_like(self.store)
         self.fitness = torch.zeros(self.P, dtype=torch.float64, device=self.device)
@@ -134,6 +147,29 @@ class DeviceGA:
         self._hof_fitness_alt = torch.zeros_like(self.hof_fitness)
         self._fit_alt = torch.zeros_like(self.fitness)
         self._summary_h = torch.zeros(8, dtype=torch.float64, pin_memory=True)
+
+    # ------------------------------------------------------------ schedule
+    def _sliced(self, n_hof: int) -> bool:
+        return self._slice is not None and n_hof >= self.hof_slices
+
+    def _opponents(self, buf: torch.Tensor, n_hof: int) -> Optional[torch.Tensor]:
+        """The hall rows this rank's games index: the whole hall, or its slice."""
+        if not n_hof:
+            return None
+        return buf[self._slice:n_hof:self.hof_slices] if self._sliced(n_hof) else buf[:n_hof]
+
+    def eval_schedule(self, g: int, n_hof: Optional[int] = None, rows="last"):
+        """(kind, opp, mult) of generation g's games for this rank's shard,
+        as the evaluation plays them (opp indexes the opponents the evaluation
+        passes -- the hall, or this rank's slice of it; rows: the evaluation
+        order, by default the last evaluation's)."""
+        n_hof = self.hof_n if n_hof is None else n_hof
+        rows = self.last_rows if isinstance(rows, str) else rows
+        kw = {}
+        if self.hof_slices > 1:
+            kw = dict(hof_slices=self.hof_slices, block_rows=self.hof_block_rows, slice_local=self._sliced(n_hof))
+        return D.schedule(self.schedule, self.hi - self.lo, self.n_games, self.lo, self.hof_fitness, n_hof, self.seed,
+                          g, self.device, rows=rows, **kw)
 
     # ------------------------------------------------------------ views
     @property
@@ -273,9 +309,8 @@ class DeviceGA:
                 dest = torch.where(inv_s, c_inv - 1, count + c_val - 1).long()
                 local = torch.empty(n, dtype=torch.int32, device=self.device)
                 local[dest] = torch.arange(lo, hi, dtype=torch.int32, device=self.device)  # invalid rows first
-        kind, opp, mult = D.schedule(self.schedule, n, self.n_games, lo, self.hof_fitness, self.hof_n,
-                                     self.seed, g, self.device, rows=local)
-        opponents = self.store[: self.hof_n] if self.hof_n else None
+        kind, opp, mult = self.eval_schedule(g, rows=local)
+        opponents = self._opponents(self.store, self.hof_n)
         out = self.last if (self.last is not None and self.last.fitness.shape[0] == n) else None
         if self.eval_events is not None:
             self.eval_events[0].record()
@@ -491,9 +526,13 @@ class DeviceGA:
         mask = self._buf("complete_" + name, self._n_pairs, torch.uint8)
         mask.zero_()
         D.mark_pairs(mask, rows, skip=self._skip, exclude=exclude)
+        # the marked pairs as a compact list: one wave per marked pair, not per pair
+        lst = self._buf("complete_list_" + name, self._n_pairs, torch.int32)  # (per name: two streams)
+        cnt = self._buf("complete_count_" + name, 1, torch.int32)
+        D.list_pairs(mask, lst, cnt)
         chosen = self._buf("chosen%d" % (g & 1), self.P, torch.int32)
         D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu, self.sigma, self.indpb,
-               seed=self.seed, generation=g, out=off, pair_mask=mask,
+               seed=self.seed, generation=g, out=off, pair_list=(lst, cnt, min(rows.numel(), self._n_pairs)),
                invalid=self._buf("complete_inv_" + name, self.P, torch.uint8))
         return mask
 
@@ -528,11 +567,10 @@ class DeviceGA:
                 or self.last.fitness.shape[0] != n):
             return None
         local, count = order
-        sched = D.schedule(self.schedule, n, self.n_games, self.lo, self.hof_fitness, self.H, self.seed, g,
-                           self.device, rows=local)
+        sched = self.eval_schedule(g, n_hof=self.H, rows=local)
         # the records land in the evaluator's workspace; the later PG_PREP_REST call
         # (same genomes, rows, count; opponents of the same size) adds the opponents'
-        self.ev.evaluate(off, *sched, opponents=self.spare[: self.H], out=self.last, validate=False,
+        self.ev.evaluate(off, *sched, opponents=self._opponents(self.spare, self.H), out=self.last, validate=False,
                          hard_log=self.hard_log, rows=local, n_active=count, prep="genomes")
         return sched
 
@@ -550,11 +588,10 @@ class DeviceGA:
         n = hi - lo
         local, count = order
         if sched is None:
-            kind, opp, mult = D.schedule(self.schedule, n, self.n_games, lo, self.hof_fitness, self.hof_n,
-                                         self.seed, g, self.device, rows=local)
+            kind, opp, mult = self.eval_schedule(g, rows=local)
         else:  # made during the hall-of-fame scan with the genomes' records (_early_prep)
             kind, opp, mult = sched
-        opponents = self.store[: self.hof_n] if self.hof_n else None
+        opponents = self._opponents(self.store, self.hof_n)
         out = self.last if (self.last is not None and self.last.fitness.shape[0] == n) else None
         if self.eval_events is not None:
             self.eval_events[0].record()

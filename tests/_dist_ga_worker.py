@@ -29,7 +29,8 @@ def main(out_dir, mode="small"):
     dev = torch.device("cuda", 0)
     if mode == "config4":
         P = 524288
-        ga = DeviceGA([6, 64, 3], P, device=dev, schedule="selfplay", seed=4)
+        # bench.py's schedule: each 65 536-row block plays its slice of the hall
+        ga = DeviceGA([6, 64, 3], P, device=dev, schedule="selfplay", seed=4, hof_block_rows=65536)
         ga.initialize("normal", 3.0)
         sample = {}
 
@@ -39,8 +40,7 @@ def main(out_dir, mode="small"):
             pick = np.sort(rng.choice(n, size=min(48, n), replace=False))
             pt = torch.as_tensor(pick, device=dev)
             r = ga.last_rows[pt].long() if ga.last_rows is not None else pt  # rows: full offspring / the shard
-            kind, opp, mult = D.schedule(ga.schedule, ga.hi - ga.lo, ga.n_games, ga.lo, ga.hof_fitness, ga.hof_n,
-                                         ga.seed, g, dev, rows=ga.last_rows)
+            kind, opp, mult = ga.eval_schedule(g)  # (opp indexes `opponents`: the hall or this rank's slice)
             o = opp[pt].cpu().numpy()
             used = np.unique(o)  # only the hall-of-fame rows these games play
             opp_rows = (opponents[torch.as_tensor(used, device=dev)].double().cpu().numpy()

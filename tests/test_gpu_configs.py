@@ -64,7 +64,6 @@ def test_config2_pop4096_device_ga_generations(gpu, oracle):
     evaluation, hall of fame; bench.py's initialisation: a full hall of
     random genomes at fitness -1e300): every evaluation's sample of played
     rows re-played by the oracle through the on_evaluate hook."""
-    from pong_amd import device as D
     from pong_amd.evolve import DeviceGA
     shape = [6, 64, 3]
     P = 4096
@@ -82,8 +81,7 @@ def test_config2_pop4096_device_ga_generations(gpu, oracle):
         pick = np.unique(np.linspace(0, played - 1, 32).astype(np.int64))
         pt = torch.as_tensor(pick, device=gpu)
         r = ga.last_rows[pt].long() if ga.last_rows is not None else pt
-        kind, opp, mult = D.schedule(ga.schedule, ga.hi - ga.lo, ga.n_games, ga.lo, ga.hof_fitness, ga.hof_n,
-                                     ga.seed, g, gpu, rows=ga.last_rows)
+        kind, opp, mult = ga.eval_schedule(g)
         o = opp[pt].cpu().numpy()
         used = np.unique(o)
         ref = oracle.eval_population(rows[r].double().cpu().numpy(), shape, kind[pt].cpu().numpy(),

@@ -30,7 +30,10 @@ def _run(world, out, *extra, timeout=240):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr=127.0.0.1", f"--master-port={_port()}", WORKER, out, *extra]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    if r.returncode != 0:  # the first rank's traceback, not just the launcher's tail
+        err = r.stderr
+        at = err.find("Traceback")
+        raise AssertionError(r.stdout[-1000:] + (err[at:at + 4000] if at >= 0 else "") + err[-2000:])
 
 
 def test_sharded_device_ga_equals_single_process(gpu, tmp_path):

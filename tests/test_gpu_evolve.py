@@ -27,6 +27,48 @@ def test_schedule_selfplay_equals_host(gpu):
         assert torch.equal(k, k2) and torch.equal(o, o2) and torch.equal(m, m2)
 
 
+@pytest.mark.parametrize("n_hof", [4096, 4099, 13])
+def test_schedule_selfplay_sliced_hall(gpu, n_hof):
+    """pg_schedule_args.hof_slices (DESIGN.md 7): row r of block b = r // B plays
+    member k * K + b of the hall, k = (r * games + g) mod |slice b| -- or k
+    itself with slice_local --, and a block evaluated against its slice alone
+    equals the same rows evaluated against the whole hall (n_hof < K: the plain
+    schedule)."""
+    from pong_amd import device as D
+    K, B, n, G6 = 4, 1000, 4000, 6
+    rows = np.arange(n)
+    k_, o, m = D.schedule("selfplay", n, G6, 0, None, n_hof, 5, 2, gpu, hof_slices=K, block_rows=B)
+    o = o.cpu().numpy()
+    if n_hof < K:
+        want = (rows[:, None] * G6 + np.arange(G6)[None, :]) % n_hof
+    else:
+        b = (rows // B) % K
+        msz = (n_hof - b + K - 1) // K
+        kk = (rows[:, None] * G6 + np.arange(G6)[None, :]) % msz[:, None]
+        want = kk * K + b[:, None]
+    np.testing.assert_array_equal(o, want)
+    if n_hof >= K:
+        _, ol, _ = D.schedule("selfplay", n, G6, 0, None, n_hof, 5, 2, gpu, hof_slices=K, block_rows=B,
+                              slice_local=True)
+        np.testing.assert_array_equal(ol.cpu().numpy(), kk)
+        # block 1's rows against slice 1 alone == against the whole hall
+        shape = [6, 64, 3]
+        G = _gene_count(shape)
+        gen = torch.Generator(device=gpu).manual_seed(n_hof)
+        genomes = torch.randn((B, G), generator=gen, dtype=torch.float64, device=gpu) * 3.0
+        hall = torch.randn((n_hof, G), generator=gen, dtype=torch.float64, device=gpu) * 3.0
+        ev = D.Evaluator(shape, device=gpu)
+        kind = torch.full((B, G6), 3, dtype=torch.int32, device=gpu)
+        mult = torch.ones((B, G6), dtype=torch.float64, device=gpu)
+        r_full, _ = ev.evaluate(genomes, kind, torch.tensor(o[B:2 * B], device=gpu), mult, opponents=hall)
+        ev2 = D.Evaluator(shape, device=gpu)
+        r_slice, _ = ev2.evaluate(genomes, kind, torch.tensor(kk[B:2 * B].astype(np.int32), device=gpu), mult,
+                                  opponents=hall[1::K])
+        torch.cuda.synchronize()
+        for name in ("fitness", "frames", "scores", "rewards"):
+            assert torch.equal(getattr(r_full, name), getattr(r_slice, name)), name
+
+
 def test_schedule_reference(gpu):
     from pong_amd import device as D
     n, H = 20000, 7

@@ -218,3 +218,35 @@ def test_vary_pair_mask_equals_full_vary(gpu, dtype):
     w = written.to(gpu)
     assert torch.equal(out[w], full[w])
     assert bool((out[~w] == 7.0).all())
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_vary_pair_list_equals_mask(gpu, dtype):
+    """pg_ga_args.pair_list (ABI 10): the marked pairs as pg_ga_list_pairs'
+    compact list give the same rows (and those rows' invalid flags) as the
+    mask, one wave per listed pair; other rows untouched."""
+    from pong_amd import device as D
+    P, G = 4001, 643
+    g = torch.Generator(device=gpu).manual_seed(6)
+    parents = torch.randn((P, G), generator=g, dtype=torch.float64, device=gpu).to(dtype)
+    chosen = torch.randint(0, P, (P,), generator=g, device=gpu, dtype=torch.int32)
+    kw = dict(cxpb=0.9, mutpb=0.9, alpha=0.9, mu=0.0, sigma=0.9, indpb=0.9, seed=4, generation=9)
+    full, inv_full = D.vary(parents, chosen, G, **kw)
+    pairs = (P + 1) // 2
+    mask = torch.zeros(pairs, dtype=torch.uint8, device=gpu)
+    rows = torch.randint(0, P, (300,), generator=g, device=gpu, dtype=torch.int32)
+    D.mark_pairs(mask, rows)
+    lst = torch.full((pairs,), -1, dtype=torch.int32, device=gpu)
+    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    D.list_pairs(mask, lst, cnt)
+    marked = mask.nonzero().flatten()
+    assert int(cnt.item()) == marked.numel()
+    assert sorted(lst[: int(cnt.item())].tolist()) == marked.tolist()
+    out = torch.full((P, G), 7.0, dtype=dtype, device=gpu)
+    inv = torch.full((P,), 9, dtype=torch.uint8, device=gpu)
+    D.vary(parents, chosen, G, **kw, out=out, invalid=inv, pair_list=(lst, cnt, rows.numel()))
+    w = torch.zeros(P, dtype=torch.bool, device=gpu)
+    for j in marked.tolist():
+        w[2 * j: min(2 * j + 2, P)] = True
+    assert torch.equal(out[w], full[w]) and bool((out[~w] == 7.0).all())
+    assert torch.equal(inv[w], inv_full[w]) and bool((inv[~w] == 9).all())

@@ -43,7 +43,8 @@ from pong_amd.evolve import DeviceGA  # noqa: E402
 
 
 def make_ga(P, dev, seed=1234, sigma=3.0):
-    ga = DeviceGA([6, 64, 3], P, device=dev, schedule="selfplay", seed=seed)
+    # bench.py's schedule: each 65 536-row block plays its slice of the hall (K = P / 65 536)
+    ga = DeviceGA([6, 64, 3], P, device=dev, schedule="selfplay", seed=seed, hof_block_rows=65536)
     ga.initialize("normal", sigma)
     gen = torch.Generator(device=dev).manual_seed(seed + 1)
     rows = max(1, (1 << 28) // (8 * ga.G))
@@ -74,12 +75,16 @@ def shard_evals(ga, n_shards):
     (ms, stepped env-steps, opponents' record prep ms) each."""
     P, S = ga.P, ga.P // n_shards
     ev = D.Evaluator(ga.nodes, dtype=ga.dtype, device=ga.device, n_games=ga.n_games, seed=ga.ev.seed)
-    opponents = ga.hall_of_fame[: ga.hof_n]
+    K = ga.hof_slices
     ms = []
     for r in range(n_shards):
         lo = r * S
+        # what rank r plays: its block's slice of the hall (bench.py's schedule)
+        sliced = K > 1 and ga.hof_n >= K and S == ga.hof_block_rows
+        opponents = ga.hall_of_fame[r % K::K] if sliced else ga.hall_of_fame[: ga.hof_n]
         kind, opp, mult = D.schedule("selfplay", S, ga.n_games, lo, ga.hof_fitness, ga.hof_n, ga.seed,
-                                     ga.generation + 1, ga.device)
+                                     ga.generation + 1, ga.device, hof_slices=K, block_rows=ga.hof_block_rows,
+                                     slice_local=sliced)
         rows = ga._rows[lo:lo + S]
         ev.evaluate(rows, kind, opp, mult, opponents=opponents, validate=False)  # warm (workspace)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -150,10 +155,14 @@ def replicated_ops(ga, n_shards=1, reps=3):
         pmask = torch.empty(pairs, dtype=torch.uint8, device=dev)
         inv = torch.empty(P, dtype=torch.uint8, device=dev)
 
-        def complete(mask, rows, exclude=None):
+        lst = torch.empty(pairs, dtype=torch.int32, device=dev)
+        cnt = torch.empty(1, dtype=torch.int32, device=dev)
+
+        def complete(mask, rows, exclude=None):  # as evolve.DeviceGA._complete: mark, list, vary the list
             mask.zero_()
             D.mark_pairs(mask, rows, skip=skip, exclude=exclude)
-            D.vary(*args, **kw, pair_mask=mask, invalid=inv)
+            D.list_pairs(mask, lst, cnt)
+            D.vary(*args, **kw, pair_list=(lst, cnt, min(rows.numel(), pairs)), invalid=inv)
         timed("complete_cand", lambda: complete(cmask, cand[:k]))
         timed("complete_parents", lambda: complete(pmask, chosen, cmask))
         out["complete_cand_pairs"] = int(cmask.sum().item())
