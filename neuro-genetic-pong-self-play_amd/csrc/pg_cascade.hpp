@@ -332,7 +332,11 @@ __device__ __forceinline__ void load_rec(NetP<U, O> &n, const float *__restrict_
 
 // Hidden layer and the lane-partial output sums of one packed network; k are
 // the six doubled-centroid features (x_i = k_i / 320 is folded into W1).
-template <int U, int O>
+// kBiasIn: n.c holds the lane's share of the output bias (k_service: half of
+// it on the group's first lane, both halves of its packed chains start from
+// it; zero elsewhere), so the group sum is z itself -- no add per output.
+// Each share passes the same roundings as a W2 term (<= out_roundings).
+template <int U, int O, bool kBiasIn = false>
 __device__ __forceinline__ void partial_pk(const NetP<U, O> &n, const int k[6], float acc[O]) {
   constexpr int P = NetP<U, O>::P;
   float2v kx[6];
@@ -343,7 +347,7 @@ __device__ __forceinline__ void partial_pk(const NetP<U, O> &n, const int k[6], 
   }
   float2v a2[O];
 #pragma unroll
-  for (int o = 0; o < O; ++o) a2[o] = float2v{0.f, 0.f};
+  for (int o = 0; o < O; ++o) a2[o] = kBiasIn ? float2v{n.c[o], n.c[o]} : float2v{0.f, 0.f};
   // two unit pairs per step: their dependent pk_fma chains interleave, so the
   // wait state a packed op owes its dependent successor is filled with work
 #pragma unroll
@@ -404,6 +408,30 @@ __device__ __forceinline__ int certify_c(const float z[O], const Cert &c) {
   const float tw = __builtin_amdgcn_exp2f(__builtin_fmaf(top1, 1.4426950408889634f, c.ee));
   const int uns_res = (top1 - top2 > c.e2 + tw && top1 > c.lowz) ? w : -1;
   return top1 >= c.tlo ? sat_res : uns_res;
+}
+
+// certify_c's decision as the action code it selects, 8 x index_to_code
+// (k_service keeps its actions so), or -1.  Three outputs: the winner's code
+// straight from the compares, and the saturated rule as "the first output at
+// or above tlo decides if it is above thi" (one select chain instead of a
+// chain per output).
+template <int O>
+__device__ __forceinline__ int certify_c8(const float z[O], const Cert &c) {
+  if constexpr (O == 3) {
+    const float top1 = fmaxf(fmaxf(z[0], z[1]), z[2]);
+    const float top2 = __builtin_amdgcn_fmed3f(z[0], z[1], z[2]);
+    const int wc = z[0] == top1 ? 8 : (z[1] == top1 ? 16 : 0);  // index_to_code8 of the first maximum
+    const float tw = __builtin_amdgcn_exp2f(__builtin_fmaf(top1, 1.4426950408889634f, c.ee));
+    const int uns_res = (top1 - top2 > c.e2 + tw && top1 > c.lowz) ? wc : -1;
+    const bool m0 = z[0] >= c.tlo, m1 = z[1] >= c.tlo;  // (with top1 >= tlo one of the three is)
+    const int fc = m0 ? 8 : (m1 ? 16 : 0);
+    const float zf = m0 ? z[0] : (m1 ? z[1] : z[2]);
+    const int sat_res = zf > c.thi ? fc : -1;
+    return top1 >= c.tlo ? sat_res : uns_res;
+  } else {
+    const int idx = certify_c<O>(z, c);
+    return idx < 0 ? -1 : index_to_code8(idx);
+  }
 }
 
 template <int O>
@@ -583,7 +611,7 @@ struct SlowSlot {
   int flag;  // 0 free, 1 posted, 2 answered (shared with the service wave: lds_ld / lds_st)
   int n_memo;  // decisions memoised for the current game's network (the owning group only)
   uint64_t memo_key[kMemo];
-  int memo_idx[kMemo];
+  int memo_idx[kMemo];  // the decision: 8 x its action code (index_to_code8)
   uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
   int rally_at, rally_span;
 };

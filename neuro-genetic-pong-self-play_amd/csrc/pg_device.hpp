@@ -42,7 +42,9 @@ constexpr int kWinScore = 3;          // WIN_SCORE config.py:53
 constexpr int kTimeoutThresh = 2000;  // TIMEOUT_THRESH config.py:28
 
 enum : int { kOppHard = 0, kOppRomCpu = 1, kOppScore = 2, kOppNN = 3 };
-enum : int { kStepFly = 0, kStepBounce = 1, kStepPoint = 2 };  // Pong::step's result
+// Pong::step's result; kStepRally: a bounce at or past the point's
+// kRallyHits-th return (PongK::step only: k_service's rally check)
+enum : int { kStepFly = 0, kStepBounce = 1, kStepPoint = 2, kStepRally = 3 };
 // k_service's serve table: game slots and points per slot (a game serves at
 // most 41 times: done() at 21 points)
 constexpr int kServeTabSlots = 16, kServeTabPoints = 64;
@@ -96,10 +98,6 @@ struct Pong {
     static_assert(kPaddleSpeed == 3, "the table below");
     return clamp_row(y + __builtin_amdgcn_sbfe(0x0003FD00, 8 * code, 8));
   }
-  // the same for a code kept as 8 x code (the table's bit offset: k_service)
-  __device__ static int move_player8(int y, int code8) {
-    return clamp_row(y + __builtin_amdgcn_sbfe(0x0003FD00, code8, 8));
-  }
 
   // env.step(action) (main.py:77): right [up,down] = action[4:6], left = action[6:8].
   // The common case -- the ball in flight, away from both paddle faces -- is
@@ -121,17 +119,12 @@ struct Pong {
   // 1-player env (k_service keeps it from its game starts: no test per frame)
   template <class ServeOf>
   __device__ int step(int right_code, int left_code, ServeOf serve_of, bool any_one_player) {
-    return step_c<false>(right_code, left_code, serve_of, any_one_player);
-  }
-  // kC8: the codes come as 8 x code (k_service keeps its actions so)
-  template <bool kC8, class ServeOf>
-  __device__ int step_c(int right_code, int left_code, ServeOf serve_of, bool any_one_player) {
     int ev = kStepFly;
-    rpy = kC8 ? move_player8(rpy, right_code) : move_player(rpy, right_code);
+    rpy = move_player(rpy, right_code);
     // left paddle: the action, or the built-in CPU of the 1-player env
     // (main.py:40) -- behind a wave-uniform test: no game of a self-play
     // schedule takes it
-    int nl = kC8 ? move_player8(lpy, left_code) : move_player(lpy, left_code);
+    int nl = move_player(lpy, left_code);
     if (__builtin_expect(any_one_player, 0)) {
       const int bc2 = 2 * by + kBallH - 1, pc2 = 2 * lpy + kPaddleH - 1;
       const int cpu_dy = vis ? ((bc2 < pc2 - 4) ? -1 : ((bc2 > pc2 + 4) ? 1 : 0)) : 0;
@@ -272,6 +265,7 @@ constexpr int kRallyStride = PG_RALLY_STRIDE;
 #define PG_RALLY_SPAN0 64
 #endif
 constexpr int kRallyHits = 8;
+static_assert(kRallyHits <= 8, "rally_key caps hits at 8");
 constexpr int kRallySpan0 = PG_RALLY_SPAN0;
 
 // Doubled centroid row of a paddle clipped to rows [0,160): what
@@ -305,6 +299,138 @@ __device__ inline int index_to_code(int idx) {  // 0 -> 1, 1 -> 2, 2, 3 -> 0: bi
 __device__ inline int index_to_code8(int idx) {  // 8 x index_to_code: byte idx of 0x1008
   return (int)__builtin_amdgcn_ubfe(0x1008u, 8u * (unsigned)idx, 8u);
 }
+
+// ---- k_service's game state: Pong in the doubled units of the features ----
+// The same game as Pong, kept as the values the networks read: the ball's
+// doubled centroid (bx2 = 2 bx + kBallW - 1, by2 = 2 by + kBallH - 1), its
+// doubled velocity, and each paddle's doubled centroid 2 py + kPaddleH - 1 --
+// so a frame's features (utils.py:139-153) need no arithmetic.  Conventions
+// of k_service that the general step does not assume:
+//  * actions as 8 x code (the move table's bit offset);
+//  * the action-driven paddles stay inside the clamp band:
+//    keep_within_game_bounds_please (utils.py:71-77, clamp_action8) forces a
+//    paddle whose top row is <= 8 (c2 <= 31) down and one whose top row is
+//    >= 137 (c2 >= 289) up, 3 rows a frame, every frame; from the reset row 72
+//    a paddle's top row stays in [6, 139] (from [9, 136] a move reaches
+//    [6, 139], from [6, 8] / [137, 139] the forced move returns it to
+//    [9, 136]; the serve-delay drift ends inside [9, 136]), where the
+//    rectangle is never clipped (c2 is the feature) and the row clamp
+//    [-8, 152] never acts.  The built-in CPU paddle of a 1-player env leaves
+//    the band: its c2 is the unclipped 2 py + 15 and c2_clip gives the feature;
+//  * a ball in play lies between the faces (bx in [lface, rface - kBallW]:
+//    served at 79, moved only while it stays there, put on a face at a
+//    bounce), so with |vx| <= kBallVxMax it can only cross the face it moves
+//    towards -- one range test, no sign tests; and the moved position is
+//    stored whatever the frame does: a bounce overwrites it, a hidden ball's
+//    position is never read (no features; the serve sets bx, by, vx and vy);
+//  * a bounce at or past the point's kRallyHits-th return reports kStepRally.
+struct PongK {
+  int bx2, by2, vx2, vy2, vis, timer, dir, hits, point, lc2, rc2, s1, s2, one_player;
+  uint64_t seed;
+  static_assert(kBallH == 4 && kPaddleH == 16 && kBallW == 2, "the doubled-unit constants below");
+  static constexpr int kC2Reset = 2 * 72 + kPaddleH - 1;
+
+  __device__ void reset(uint64_t s, int one_p) {
+    bx2 = 2 * 79 + kBallW - 1; by2 = 2 * 78 + kBallH - 1; vx2 = 0; vy2 = 0; vis = 0; timer = kServeDelay;
+    dir = 1; hits = 0; point = 0; lc2 = kC2Reset; rc2 = kC2Reset; s1 = 0; s2 = 0; one_player = one_p; seed = s;
+  }
+  __device__ bool done() const { return s1 >= kDoneScore || s2 >= kDoneScore; }
+
+  // the feature of a paddle centroid kept unclipped (the 1-player CPU paddle)
+  __device__ static int c2_clip(int c2) { return paddle_c2((c2 - (kPaddleH - 1)) >> 1); }
+  // Pong::drift in centroid units: top row <= 8 <=> c2 <= 31, >= 137 <=> c2 >= 289;
+  // (11 - py) / 3 = (37 - c2) / 6 and (py - 134) / 3 = (c2 - 283) / 6 (c2 odd)
+  __device__ static int drift2(int c2, int h) {
+    const int down = c2 <= 31 ? min((37 - c2) / 6, h) : 0;
+    const int up = c2 >= 289 ? min((c2 - 283) / 6, h) : 0;
+    return c2 + 2 * kPaddleSpeed * (down - up);
+  }
+
+  // env.step (Pong::step) on 8 x codes; serve_of(point) = Pong::serve_entry(seed, point)
+  template <class ServeOf>
+  __device__ int step(int right8, int left8, ServeOf serve_of, bool any_one_player) {
+    static_assert(kPaddleSpeed == 3, "the table below: 0, -6, +6, 0 half-rows");
+    int ev = kStepFly;
+    rc2 += __builtin_amdgcn_sbfe(0x0006FA00, right8, 8);
+    int nl = lc2 + __builtin_amdgcn_sbfe(0x0006FA00, left8, 8);
+    if (__builtin_expect(any_one_player, 0)) {  // the 1-player env's CPU (main.py:40), Pong::step's rule
+      const int cpu_dy = vis ? ((by2 < lc2 - 4) ? -1 : ((by2 > lc2 + 4) ? 1 : 0)) : 0;
+      const int moved = lc2 + 2 * kCpuSpeed * cpu_dy;
+      constexpr int lo = 2 * kPaddleYMin + kPaddleH - 1, hi = 2 * kPaddleYMax + kPaddleH - 1;
+      nl = one_player ? (moved < lo ? lo : (moved > hi ? hi : moved)) : nl;
+    }
+    lc2 = nl;
+
+    constexpr int top2 = kBallH - 1;                              // ny < 0    <=> ny2 < top2
+    constexpr int bot2 = 2 * (kFieldH - kBallH) + kBallH - 1;     // ny > ymax <=> ny2 > bot2
+    constexpr int lface = kLeftPaddleX + kPaddleW, rface = kRightPaddleX;
+    constexpr int left2 = 2 * (lface - 1) + kBallW - 1;           // nx <= lface - 1
+    constexpr int right2 = 2 * (rface - kBallW + 1) + kBallW - 1; // nx + kBallW - 1 >= rface
+    const bool play = vis != 0;
+    const int nx2 = bx2 + vx2;
+    int ny2 = by2 + vy2;
+    const bool wall_top = ny2 < top2, wall_bot = ny2 > bot2;
+    ny2 = wall_top ? 2 * top2 - ny2 : (wall_bot ? 2 * bot2 - ny2 : ny2);  // -ny, 2 ymax - ny
+    vy2 = (wall_top || wall_bot) ? -vy2 : vy2;
+    const bool to_left = play && nx2 <= left2;
+    const bool to_right = play && nx2 >= right2;
+    bx2 = nx2;
+    by2 = ny2;
+    if (PG_ANY(to_left || to_right || !play)) {
+    if (to_left || to_right) {  // crossing a paddle face: bounce or miss
+      // d = 2 (ny - py) - 12; the rows overlap iff -3 <= ny - py <= 15
+      const int d = ny2 - (to_left ? lc2 : rc2);
+      if (d >= -18 && d <= 18) {  // bounce
+        hits += 1;
+        const int mag = min(kBallVx0 + (hits >> 2), kBallVxMax);
+        const int q = (abs(d) * 43) >> 8;  // |d| / 6 for even |d| <= 18
+        bx2 = to_left ? 2 * lface + kBallW - 1 : 2 * (rface - kBallW) + kBallW - 1;
+        vx2 = to_left ? 2 * mag : -2 * mag;
+        vy2 = d < 0 ? -2 * q : 2 * q;
+        ev = hits >= kRallyHits ? kStepRally : kStepBounce;
+      } else {  // a miss scores for the other side; the ball is hidden until the next serve
+        s2 += to_left ? 1 : 0;
+        s1 += to_right ? 1 : 0;
+        dir = to_left ? -1 : 1;
+        timer = kServeDelay;
+        vis = 0;
+        ev = kStepPoint;
+      }
+    }
+    if (!play) {
+      timer = timer > 0 ? timer - 1 : 0;
+      if (timer == 0 && !done()) {
+        const uint32_t e = serve_of(point);
+        bx2 = 2 * 79 + kBallW - 1;
+        by2 = 2 * (int)(e & 255u) + kBallH - 1;
+        vy2 = 2 * ((int)(e >> 8) - 2);
+        vx2 = 2 * dir * kBallVx0;
+        hits = 0;
+        vis = 1;
+        point += 1;
+      }
+    }
+    }
+    return ev;
+  }
+
+  // rally_key of the same state (Pong units)
+  __device__ uint64_t key(int act_r, int act_l) const {
+    Pong s;
+    s.bx = (bx2 - (kBallW - 1)) >> 1;
+    s.by = (by2 - (kBallH - 1)) >> 1;
+    s.vx = vx2 >> 1;
+    s.vy = vy2 >> 1;
+    s.vis = vis;
+    s.timer = timer;
+    s.dir = dir;
+    s.hits = hits;
+    s.point = point;
+    s.lpy = (lc2 - (kPaddleH - 1)) >> 1;
+    s.rpy = (rc2 - (kPaddleH - 1)) >> 1;
+    return rally_key(s, act_r, act_l);
+  }
+};
 
 // ---- wave-level helpers ----
 template <int CTRL>

@@ -77,7 +77,9 @@ __device__ inline int genome_row(const EvalParams &p, int i) { return p.rows ? p
 
 // Results of one finished game: perform_episode's return value and the
 // bookkeeping around it (main.py:108-112, utils.py:104-109).
-__device__ inline double episode_reward(const Pong &st, int total, double mult, int &zero_div) {
+// (S: Pong or PongK; only the scores are read)
+template <class S>
+__device__ inline double episode_reward(const S &st, int total, double mult, int &zero_div) {
   zero_div = 0;
   if (st.s1 == st.s2) return 0.0;  // main.py:109-110
   const double tf = (double)total;
@@ -91,7 +93,8 @@ __device__ inline double episode_reward(const Pong &st, int total, double mult, 
   return __dadd_rn(diff, bonus) / (tf / 100.0);
 }
 
-__device__ inline void finish_game(const EvalParams &p, int w, const Pong &st, int frames, int total) {
+template <class S>
+__device__ inline void finish_game(const EvalParams &p, int w, const S &st, int frames, int total) {
   int zero_div;
   const double reward = episode_reward(st, total, p.mult[w], zero_div);
   p.rewards[w] = reward;

@@ -21,6 +21,9 @@ namespace pg {
 // requests the service wave decides together (fast_f64_decide_batch).  1 in
 // the product: batches of 4 measured neutral (profiles/r04/sweep_svc_batch_a6.log)
 // and their arrays count against every wave's register allocation (round-5 review)
+#ifndef PG_SVC_PRIO
+#define PG_SVC_PRIO 3
+#endif
 #ifndef PG_SVC_BATCH
 #define PG_SVC_BATCH 1
 #endif
@@ -123,6 +126,11 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 
   if (wave == kSvcGameWaves) {
     // ---------------- service wave: f64 re-decisions for the whole block ----
+    // the service wave's issue priority over its SIMD partner (a game wave):
+    // an answer sooner is a requester's wait shorter (PG_SVC_PRIO 3 vs 0,
+    // same box: the driver's bench +4 %, one launch of the sweep neutral,
+    // profiles/r05/bench_ab_b6.log, sweep_ab_b6.log)
+    if constexpr (PG_SVC_PRIO > 0) __builtin_amdgcn_s_setprio(PG_SVC_PRIO);
     // requests taken together (H <= 64 layouts: one hidden unit per lane)
     constexpr int kSvcBatch = U * HL <= 64 ? PG_SVC_BATCH : 1;
     const WT *genomes_svc = (const WT *)p.genomes;
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   const WT *opponents = (const WT *)p.opponents;
 
   NetP<U, O> net;
-  Pong st;
+  PongK st;  // the game in the features' doubled units (pg_device.hpp)
   // Frame bookkeeping against a wave-scalar frame counter (every lane of the
   // loop steps one frame per iteration): a game's frames = sframe - fstart, its
   // no-score counter (main.py:128-135) = sframe - (tend - TIMEOUT_THRESH), so a
@@ -233,8 +241,17 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   // (main.py:102-107) change only at a point, inside the rare block
   // act_r / act_l: the actions written into action[4:6] / [6:8] (main.py:91-92)
   // as 8 x code (code 0 = [0,0], 1 = up, 2 = down), the next step's table offset
+  // c_vis: the game's visible frames (a forward each), counted per frame --
+  // or, kVisByFrames, the frame counter at its start: an instance that
+  // advances every hidden serve delay at once steps exactly one hidden frame
+  // per point (the miss), so visible = iterations - points, taken at the end
   int kind = 0, act_r = 0, act_l = 0, total = 0, fstart = 0, tend = 0, c_vis = 0, tab_off = 0;
   int sframe = 0;
+#ifndef PG_NO_HIDDEN_JUMP
+  constexpr bool kVisByFrames = kUntraced && !kHorizon;
+#else
+  constexpr bool kVisByFrames = false;
+#endif
   const WT *gm = genomes;
   uint32_t slow = 0, c_fwd = 0, c_steps = 0, c_games = 0, fails = 0, plateau = 0, inwave = 0, skipped = 0, hidden = 0;
 
@@ -271,7 +288,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #else
 #define PG_PP(cnt, cond)
 #endif
-  while (w < games_total) {
+  // a group leaves the loop at its game-end block when the queue is empty (no per-frame test)
+  if (w < games_total) for (;;) {
 #ifdef PG_START_PROBE
     const bool any_fresh = __builtin_amdgcn_ballot_w64(fresh) != 0;
     const uint64_t probe_f0 = __builtin_amdgcn_s_memtime();
@@ -297,13 +315,18 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       const int oj = nn ? min(max(p.opp[w], 0), p.n_opponents - 1) : 0;
       gm = nn ? opponents + (long)oj * p.ostride : gr;
       load_rec<U, O>(net, p.recs + ((nn ? (long)p.n_genomes + oj : (long)i) * HL + hl) * rec_floats<U, O>());
+      // the output bias enters the first lane's two partial chains, half each
+      // (exact), so the frame adds no bias after the group sum (partial_pk)
+#pragma unroll
+      for (int o = 0; o < O; ++o) net.c[o] = hl == 0 ? 0.5f * net.c[o] : 0.f;
       st.reset(0, kind == kOppRomCpu);
       // the slot's serve seed: the LDS table holds a tabbed slot's first
       // kServeTabPoints serves; a horizon slot carries its point count across
       // auto-resets past them, where the step falls back to serve_entry(seed, pt)
       if (kHorizon || !tabbed) st.seed = game_seed(p.seed, g);  // (a wave-uniform test)
       tab_off = g * kServeTabPoints;
-      act_r = act_l = total = c_vis = 0;
+      act_r = act_l = total = 0;
+      c_vis = kVisByFrames ? sframe - 1 : 0;
       fstart = sframe - 1;             // this iteration is the game's frame 1
       tend = sframe + kTimeoutThresh;  // frame 1 does not count (main.py:94-96): it takes the counter to 0
       fresh = false;
@@ -334,11 +357,11 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       PG_PP(pp_hidden, hid);
       if (kJumps && hid) {
         const int h = st.timer - 1;
-        st.rpy = Pong::drift(st.rpy, h);
-        if (!st.one_player) st.lpy = Pong::drift(st.lpy, h);
+        st.rc2 = PongK::drift2(st.rc2, h);
+        if (!st.one_player) st.lc2 = PongK::drift2(st.lc2, h);
         st.timer = 1;
-        act_r = clamp_action8(paddle_c2(st.rpy), 0);
-        act_l = clamp_action8(paddle_c2(st.lpy), 0);
+        act_r = clamp_action8(st.rc2, 0);
+        act_l = clamp_action8(st.lc2, 0);  // (a 1-player env's CPU paddle: unclipped, the same side of the band)
         fstart -= h;  // frames += h, and the no-score counter with them
         tend -= h;
         hidden += h;
@@ -351,50 +374,59 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     w_onep = PG_ANY(st.one_player != 0);
     top = false;  // every start and serve delay above is done
     }
-    const int pvis = st.vis, pbx2 = 2 * st.bx + kBallW - 1, pby2 = 2 * st.by + kBallH - 1;
+    const int pvis = st.vis, pbx2 = st.bx2, pby2 = st.by2;
 #ifdef PG_PATH_PROBE
     const int pt_b = st.point, hits_b = st.hits;
 #endif
-    const int ev = st.template step_c<true>(act_r, act_l, [&](int pt) {
+    const int ev = st.step(act_r, act_l, [&](int pt) {
       return tabbed && pt < kServeTabPoints ? serve_tab[tab_off + pt] : Pong::serve_entry(st.seed, pt);
     }, w_onep);
-    const bool bounced = ev == kStepBounce;  // a paddle returned the ball this frame
     PG_PP(pp_face, ev != kStepFly || st.hits != hits_b || st.point != pt_b);
     const int vis = st.vis;
-    const int bx2 = 2 * st.bx + kBallW - 1, by2 = 2 * st.by + kBallH - 1;
-    const int lc2 = paddle_c2(st.lpy), rc2 = paddle_c2(st.rpy);
-    int left = 0, right = 0;
-    if (vis) {  // get_actions main.py:143-150; features utils.py:139-153
+    const int bx2 = st.bx2, by2 = st.by2;
+    // the paddles' centroids: inside the clamp band, the features themselves
+    const int rc2 = st.rc2;
+    int lc2 = st.lc2;
+    if (__builtin_expect(w_onep, 0)) lc2 = PongK::c2_clip(st.lc2);  // the built-in CPU's paddle leaves it
+    int left, right;
+    // get_actions main.py:143-150; features utils.py:139-153.  The networks run
+    // in every lane: a stepped frame with the ball hidden is rare (the miss
+    // frame of a point, when the serve delays are advanced at once), so the
+    // wave runs the block anyway, and such a lane's decision is [0,0]
+    // (main.py:151-153) -- one select instead of a branch and two moves
+    {
       const int lbx2 = pvis ? pbx2 : bx2, lby2 = pvis ? pby2 : by2;
       // [bx, by, lbx, lby, me = right, enemy = left] for both halves: the left
       // network's x-flip and me/enemy swap (main.py:146-147) are in its weights
       const int k[6] = {bx2, by2, lbx2, lby2, rc2, lc2};
       float acc[O], z[O];
-      partial_pk<U, O>(net, k, acc);
+      partial_pk<U, O, true>(net, k, acc);
 #pragma unroll
-      for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
-      int idx = certify_c<O>(z, net.ct);
+      for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]);
+      int code = certify_c8<O>(z, net.ct);  // the decision as 8 x its action code, or -1
 #ifdef PG_PROBE_EXTRA  // timing-only experiment build: extra instructions of one class every visible frame
       pg_probe_extra<PG_PROBE_EXTRA>(net.w1[0][0], net.w1[1][1], z[0], z[1], probe_v, probe_p, probe_s);
 #endif
       const bool left_nn = kind == kOppNN;
-      if (side && !left_nn) idx = 0;  // the left half is idle against a scripted opponent
+      if (side && !left_nn) code = 8;  // the left half is idle against a scripted opponent
+      if (!vis) code = 0;
 #ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
-      if (idx < 0) idx = z[1] > z[0] ? 1 : 0;
+      if (code < 0) code = z[1] > z[0] ? 16 : 8;
 #endif
-      PG_PP(pp_fail, idx < 0);
+      PG_PP(pp_fail, code < 0);
       // rare, half-uniform: the in-wave plateau rule, then the memo, else ask
       // the service wave (one wave-uniform test on the common path)
-      if (PG_ANY(idx < 0)) {
-      if (idx < 0) {
+      if (PG_ANY(code < 0)) {
+      if (code < 0) {
         fails += 1;
 #ifdef PG_TIMELINE
         g_fails += 1;
 #endif
-        idx = plateau_f32<O>(z, net.e);
+        const int idx = plateau_f32<O>(z, net.e);
         inwave += idx >= 0 ? 1 : 0;
+        code = idx >= 0 ? index_to_code8(idx) : -1;
       }
-      if (PG_ANY(idx < 0) && idx < 0) {
+      if (PG_ANY(code < 0) && code < 0) {
         const uint64_t key = memo_key(k);
         const int nm = slots[sx].n_memo;
         int hit = -1;
@@ -402,7 +434,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         for (int c = 0; c < kMemo && c < nm; ++c)
           if (slots[sx].memo_key[c] == key) hit = slots[sx].memo_idx[c];
         if (hit != -1) {
-          idx = hit;
+          code = hit;
         } else {
           if (hl == 0) {
             // the network's own features (x-flipped for the left paddle): the f64 path uses the genes
@@ -426,28 +458,28 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           g_slow += 1;  // service round trips
 #endif
           plateau += ans >> 9;
-          idx = ans & 255;
+          code = index_to_code8(ans & 255);
           if (hl == 0) {
             const int c = nm % kMemo;  // round-robin replacement
             slots[sx].memo_key[c] = key;
-            slots[sx].memo_idx[c] = idx;
+            slots[sx].memo_idx[c] = code;
             slots[sx].n_memo = nm + 1;
             lds_st(&slots[sx].flag, 0);
           }
         }
       }
       }
-      const int mine = index_to_code8(idx);
+      const int mine = code;
       const int other = other_half<L>(mine);
       right = side ? other : mine;
       left = side ? mine : other;
       // HardcodedAi / ScoreHardcodedAi (dumb_ais.py): behind a wave-uniform
       // test, which a self-play schedule never passes
       if (__builtin_expect(w_scripted, 0) && !left_nn) {
-        left = hardcoded8(by2, lc2);
+        left = vis ? hardcoded8(by2, lc2) : 0;
         if (kind == kOppScore && st.s1 > st.s2) left = 0;
       }
-      c_vis += 1;  // forwards: c_vis x (1 or 2 networks), counted at the game's end
+      if constexpr (!kVisByFrames) c_vis += vis;  // forwards: c_vis x (1 or 2 networks), counted at the game's end
     }
     act_l = clamp_action8(lc2, left);
     act_r = clamp_action8(rc2, right);
@@ -480,7 +512,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // opening at the 8th return instead of at timeout 256, with a 64-frame
     // first span, fires at the cycle's first repetition in the common
     // two-bounce rally (tools/long_games.py: 460 instead of 610 frames).
-    const bool rally_check = !kTracing && !kHorizon && bounced && st.hits >= kRallyHits;
+    const bool rally_check = !kTracing && !kHorizon && ev == kStepRally;  // (step_c<true>: hits >= kRallyHits)
 #else
     constexpr bool rally_check = false;
 #endif
@@ -489,7 +521,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     bool over = sframe > tend;
     if constexpr (kHorizon) over = over || sframe - fstart >= p.horizon;
     // a point, a rally check or a game end: one wave-uniform test on the common path
-    if (PG_ANY(!same || rally_check || over)) {
+    // (a bounce past the kRallyHits-th return enters it even when the rally
+    // check is off, tracing: one compare on the common path instead of three)
+    if (PG_ANY((kHorizon ? !same : ev >= kStepPoint) || over)) {
     if (!same) {  // a point: total_frames += timeout, timeout = 0 (main.py:128-135); the scores' end test
       total += sframe - 1 - (tend - kTimeoutThresh);
       tend = sframe + kTimeoutThresh;
@@ -500,7 +534,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     const int timeout = sframe - (tend - kTimeoutThresh);
     if (rally_check && timeout <= kTimeoutThresh) {
       const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
-      const uint64_t key = rally_key(st, act_r >> 3, act_l >> 3);
+      const uint64_t key = st.key(act_r >> 3, act_l >> 3);
       const int at = slots[rs].rally_at;
       if (at > timeout || at < 0) {
         if (lig == 0) {
@@ -575,11 +609,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       }
 #endif
       c_steps += sframe - fstart;
-      c_fwd += (kind == kOppNN ? 2u : 1u) * (uint32_t)c_vis;
+      const int vis_frames = kVisByFrames ? sframe - c_vis - (st.s1 + st.s2) : c_vis;
+      c_fwd += (kind == kOppNN ? 2u : 1u) * (uint32_t)vis_frames;
       c_games += 1;
       int ww = 0;
       if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
       w = group_broadcast<L>(ww, leader);
+      if (w >= games_total) break;
       fresh = true;
     }
     // what the next frame's top block has to do: a start, or (a point) a serve delay to advance

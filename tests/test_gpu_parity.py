@@ -211,6 +211,35 @@ def test_eval_near_saturation_matches_oracle(gpu, oracle):
     assert c[2] + c[5] + c[6] <= c[4], c           # each failure is decided once
 
 
+def test_eval_forward_count_by_frames(gpu, oracle):
+    """The bench instance (8-lane groups, untraced) counts a game's forwards
+    from its frame counter -- one hidden frame stepped per point, so visible
+    frames = stepped frames - points -- while the other layouts count every
+    visible frame: on a self-play launch the two agree with each other and
+    with 2 x (stepped frames - points), and the results with the oracle."""
+    from pong_amd.device import Evaluator
+    shape = [6, 64, 3]
+    rng = np.random.default_rng(17)
+    G = _gene_count(shape)
+    n, H = 384, 128
+    genomes = rng.standard_normal((n, G)) * 3.0
+    opponents = rng.standard_normal((H, G)) * 3.0
+    kinds = np.full((n, 6), 3, np.int32)
+    opp = rng.integers(0, H, size=(n, 6)).astype(np.int32)
+    mult = np.ones((n, 6))
+    counters = []
+    for lanes in (8, 16):
+        ev = Evaluator(shape, device=gpu, group_lanes=lanes, kernel="split")
+        res, ref = _run_both(ev, oracle, genomes, opponents, kinds, opp, mult, gpu)
+        _assert_same(res, ref)
+        c = res.counters.cpu().numpy().astype(np.int64)
+        points = int(res.scores.sum())
+        assert c[1] == 2 * (c[0] - points), (lanes, c[0], c[1], points)
+        counters.append(c)
+    for i in (0, 1, 3, 8, 12):  # stepped frames, forwards, games, rally-skipped, hidden-jumped
+        assert counters[0][i] == counters[1][i], (i, counters)
+
+
 def test_eval_f32_genomes(gpu, oracle):
     """f32 genome storage: the oracle sees the same f32-rounded genes."""
     from pong_amd.device import Evaluator
