@@ -410,8 +410,8 @@ __device__ __forceinline__ int certify_c(const float z[O], const Cert &c) {
   return top1 >= c.tlo ? sat_res : uns_res;
 }
 
-// certify_c's decision as the action code it selects, 8 x index_to_code
-// (k_service keeps its actions so), or -1.  Three outputs: the winner's code
+// certify_c's decision as the paddle move it selects (index_to_move:
+// k_service keeps its actions so), or -1 (no move is -1).  Three outputs: the winner's code
 // straight from the compares, and the saturated rule as "the first output at
 // or above tlo decides if it is above thi" (one select chain instead of a
 // chain per output).
@@ -420,17 +420,27 @@ __device__ __forceinline__ int certify_c8(const float z[O], const Cert &c) {
   if constexpr (O == 3) {
     const float top1 = fmaxf(fmaxf(z[0], z[1]), z[2]);
     const float top2 = __builtin_amdgcn_fmed3f(z[0], z[1], z[2]);
-    const int wc = z[0] == top1 ? 8 : (z[1] == top1 ? 16 : 0);  // index_to_code8 of the first maximum
+    const int wc = z[0] == top1 ? -6 : (z[1] == top1 ? 6 : 0);  // index_to_move of the first maximum
     const float tw = __builtin_amdgcn_exp2f(__builtin_fmaf(top1, 1.4426950408889634f, c.ee));
-    const int uns_res = (top1 - top2 > c.e2 + tw && top1 > c.lowz) ? wc : -1;
+#ifndef PG_CERT_FULL_SAT
+    // saturated: decided here only when the winner is the one output that may
+    // be saturated (top2 < tlo) and surely is; two or more maybe-saturated
+    // outputs (ties at 1.0 in f64) are left to the plateau rule (plateau_f32)
+    // (bitwise on the compares: lane masks, no divergent branches; top1 > thi
+    // implies top1 >= tlo, the saturated regime)
+    const bool ok = ((top2 < c.tlo) & (top1 > c.thi)) | ((top1 < c.tlo) & (top1 - top2 > c.e2 + tw) & (top1 > c.lowz));
+    return ok ? wc : -1;
+#else
     const bool m0 = z[0] >= c.tlo, m1 = z[1] >= c.tlo;  // (with top1 >= tlo one of the three is)
     const int fc = m0 ? 8 : (m1 ? 16 : 0);
     const float zf = m0 ? z[0] : (m1 ? z[1] : z[2]);
     const int sat_res = zf > c.thi ? fc : -1;
+    const int uns_res = (top1 - top2 > c.e2 + tw && top1 > c.lowz) ? wc : -1;
     return top1 >= c.tlo ? sat_res : uns_res;
+#endif
   } else {
     const int idx = certify_c<O>(z, c);
-    return idx < 0 ? -1 : index_to_code8(idx);
+    return idx < 0 ? -1 : index_to_move(idx);
   }
 }
 
@@ -592,6 +602,15 @@ __host__ __device__ constexpr int svc_threads() {
 // of (network, features), so a hit is exact.  Cleared at every game start.
 constexpr int kMemo = 8;
 
+// The lane's index in its wave, computed afresh (volatile: never hoisted or
+// merged), for lane values a rare block needs but the hot loop should not
+// keep live.
+__device__ __forceinline__ int fresh_lane64() {
+  int r;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+  return r;
+}
+
 // Relaxed workgroup-scope atomics on LDS words that another wave polls.  Not
 // `volatile`: a volatile access through the generic pointer of a __shared__
 // variable is not rewritten to LDS and becomes a flat access (sc0 sc1, a trip
@@ -611,9 +630,10 @@ struct SlowSlot {
   int flag;  // 0 free, 1 posted, 2 answered (shared with the service wave: lds_ld / lds_st)
   int n_memo;  // decisions memoised for the current game's network (the owning group only)
   uint64_t memo_key[kMemo];
-  int memo_idx[kMemo];  // the decision: 8 x its action code (index_to_code8)
+  int memo_idx[kMemo];  // the decision: its paddle move (index_to_move)
   uint64_t rally_key;  // Brent's saved rally key of the slot's game (side-0 slot of a group)
   int rally_at, rally_span;
+  int rec;  // k_service inline form: the slot's network's lane-record index (its reload after a decision)
 };
 
 // fixed-horizon mode (pg_eval_args.horizon), one per game group: the completed

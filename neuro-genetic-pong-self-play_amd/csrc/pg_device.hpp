@@ -281,23 +281,28 @@ __device__ inline int paddle_c2(int py) {
 __device__ inline int clamp_action(int c2, int code) {
   return c2 < 32 ? 2 : (c2 > 2 * (kFieldH - 16) ? 1 : code);
 }
-__device__ inline int clamp_action8(int c2, int code8) {  // the same on 8 x code
-  return c2 < 32 ? 16 : (c2 > 2 * (kFieldH - 16) ? 8 : code8);
+// The same on k_service's actions, kept as the paddle's move in centroid
+// units (doubled rows): up -6, down +6, no-op 0 -- the step adds it as is.
+__device__ inline int clamp_move(int c2, int move) {
+  static_assert(kPaddleSpeed == 3, "doubled moves of 6");
+  return c2 < 32 ? 6 : (c2 > 2 * (kFieldH - 16) ? -6 : move);
 }
+// the action code (1 up, 2 down, 0 none) of a move: the trace and rally_key
+__device__ inline int move_code(int move) { return move < 0 ? 1 : (move > 0 ? 2 : 0); }
 
 // HardcodedAi.run (dumb_ais.py:2-8) on inference() features: compares
 // ball_y/160 (x[1]) with me/160 (x[4]); the /160 is monotone, so the doubled
 // integer centroids compare the same way.
 __device__ inline int hardcoded(int by2, int me2) { return by2 < me2 ? 1 : (by2 > me2 ? 2 : 0); }
-__device__ inline int hardcoded8(int by2, int me2) { return by2 < me2 ? 8 : (by2 > me2 ? 16 : 0); }
+__device__ inline int hardcoded_move(int by2, int me2) { return by2 < me2 ? -6 : (by2 > me2 ? 6 : 0); }
 
 // argmax index -> action code (numpy_nn.py:131-137; index >= 2 -> no-op, the
 // build's extension for 3-output networks).
 __device__ inline int index_to_code(int idx) {  // 0 -> 1, 1 -> 2, 2, 3 -> 0: bits 2 idx of 0b1001
   return (int)__builtin_amdgcn_ubfe(9u, 2u * (unsigned)idx, 2u);
 }
-__device__ inline int index_to_code8(int idx) {  // 8 x index_to_code: byte idx of 0x1008
-  return (int)__builtin_amdgcn_ubfe(0x1008u, 8u * (unsigned)idx, 8u);
+__device__ inline int index_to_move(int idx) {  // clamp_move's units: signed byte idx of 0x0006FA
+  return (int)__builtin_amdgcn_sbfe(0x0006FA, 8u * (unsigned)idx, 8u);
 }
 
 // ---- k_service's game state: Pong in the doubled units of the features ----
@@ -306,9 +311,9 @@ __device__ inline int index_to_code8(int idx) {  // 8 x index_to_code: byte idx 
 // doubled velocity, and each paddle's doubled centroid 2 py + kPaddleH - 1 --
 // so a frame's features (utils.py:139-153) need no arithmetic.  Conventions
 // of k_service that the general step does not assume:
-//  * actions as 8 x code (the move table's bit offset);
+//  * actions as the paddle's move in centroid units (clamp_move: -6, 0, +6);
 //  * the action-driven paddles stay inside the clamp band:
-//    keep_within_game_bounds_please (utils.py:71-77, clamp_action8) forces a
+//    keep_within_game_bounds_please (utils.py:71-77, clamp_move) forces a
 //    paddle whose top row is <= 8 (c2 <= 31) down and one whose top row is
 //    >= 137 (c2 >= 289) up, 3 rows a frame, every frame; from the reset row 72
 //    a paddle's top row stays in [6, 139] (from [9, 136] a move reaches
@@ -346,13 +351,12 @@ struct PongK {
     return c2 + 2 * kPaddleSpeed * (down - up);
   }
 
-  // env.step (Pong::step) on 8 x codes; serve_of(point) = Pong::serve_entry(seed, point)
+  // env.step (Pong::step) on the paddles' moves; serve_of(point) = Pong::serve_entry(seed, point)
   template <class ServeOf>
-  __device__ int step(int right8, int left8, ServeOf serve_of, bool any_one_player) {
-    static_assert(kPaddleSpeed == 3, "the table below: 0, -6, +6, 0 half-rows");
+  __device__ int step(int right_move, int left_move, ServeOf serve_of, bool any_one_player) {
     int ev = kStepFly;
-    rc2 += __builtin_amdgcn_sbfe(0x0006FA00, right8, 8);
-    int nl = lc2 + __builtin_amdgcn_sbfe(0x0006FA00, left8, 8);
+    rc2 += right_move;
+    int nl = lc2 + left_move;
     if (__builtin_expect(any_one_player, 0)) {  // the 1-player env's CPU (main.py:40), Pong::step's rule
       const int cpu_dy = vis ? ((by2 < lc2 - 4) ? -1 : ((by2 > lc2 + 4) ? 1 : 0)) : 0;
       const int moved = lc2 + 2 * kCpuSpeed * cpu_dy;

@@ -28,6 +28,58 @@ namespace pg {
 #define PG_SVC_BATCH 1
 #endif
 
+// The bench layout (L = 8, U = 16, not the fixed-horizon mode) decides its
+// certificate failures inside the game wave (kInline): the whole wave takes
+// the still-undecided half-groups one at a time (serve_inline) instead of a
+// dedicated service wave answering through an LDS mailbox.  A requester
+// waited for its answer either way; the service wave's slot becomes an
+// eighth game wave -- two game waves on every SIMD, where the service wave's
+// SIMD had one.  PG_INLINE_SVC=0 builds the service-wave form (A/B).
+#ifndef PG_INLINE_SVC
+#define PG_INLINE_SVC 1
+#endif
+// the deciding wave's issue priority over its SIMD partner while it decides
+// (3 vs 0, same box: the driver's bench 11.40 / 11.46 vs 11.36 / 11.13 ·10^9,
+// one sweep launch equal; profiles/r05/bench_ab_b7.log)
+#ifndef PG_INLINE_PRIO
+#define PG_INLINE_PRIO 3
+#endif
+template <int L, int U, bool kHorizon>
+__host__ __device__ constexpr bool inline_service() {
+  return PG_INLINE_SVC && L == 8 && U == 16 && !kHorizon;
+}
+
+// One request, by the whole wave (every lane active): the f32 outputs'
+// plateau rule, else the certified f64 decision, else numpy's own order in
+// f64 (lds: this wave's f64_lds_doubles(H, O) scratch).  The answer as the
+// service wave's: the index, bit 8 numpy-order, bit 9 certified.  Not
+// inlined: its registers are the callee's, saved around the call on this
+// rare path, not added to the game loop's budget.
+struct InlineReq {
+  int k[6];
+  float z[4];
+  float e;
+};
+template <int U, int HL, int O, typename WT>
+__device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, InlineReq r, double *lds,
+                                                      int lane64) {
+  const int H = p.nodes[1];
+  const int b = p.bias;
+  float zf[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) zf[o] = r.z[o];
+  int d = plateau_decide<O>(zf, r.e, lane64);
+  if (d < 0) d = fast_f64_decide<O, WT>(g, H, b, r.k, lane64);
+  if (d >= 0) return d | 512;
+  d = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, r.k, lds, lane64);
+  if (p.hard_log && lane64 == 0) {
+    const long oo = g - (const WT *)p.opponents;
+    const bool opp = p.opponents != p.genomes && oo >= 0 && oo < (long)p.n_opponents * p.ostride;
+    log_hard(p, (int)(opp ? oo / p.ostride : (g - (const WT *)p.genomes) / p.gstride), opp ? 1 : 0, d, 0, r.k);
+  }
+  return d | 256;
+}
+
 // Every network a launch plays, once, in the layout a game lane holds it
 // (load_net_pk: pre-scaled f32 weights, the left paddle's x-flip folded in,
 // the certificate's bound): record r < n_genomes is entry r's genome as the
@@ -96,7 +148,9 @@ __device__ __forceinline__ void pg_probe_extra(float2v w, float2v w2, float a, f
 template <int L, int U, int O, typename WT, bool kUntraced = false, bool kHorizon = false>
 __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   constexpr int kSvcThreads = svc_threads<U>();
-  constexpr int kSvcGameWaves = kSvcThreads / 64 - 1;
+  constexpr bool kInline = inline_service<L, U, kHorizon>();
+  static_assert(!kInline || O <= 4, "InlineReq.z");
+  constexpr int kSvcGameWaves = kSvcThreads / 64 - (kInline ? 0 : 1);
   constexpr int HL = L / 2;
   constexpr int kSlots = kSvcGameWaves * (64 / L) * 2;
   __shared__ SlowSlot slots[kSlots];
@@ -108,12 +162,15 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   // slot's physics seed and the point): a serve is one ds_read instead of a
   // splitmix64 and a 64-bit remainder; launches with more slots compute them
   __shared__ uint32_t serve_tab[kServeTabSlots * kServeTabPoints];
-  extern __shared__ double lds_svc[];  // f64_lds_doubles(H, O), service wave only
+  extern __shared__ double lds_svc[];  // f64_lds_doubles(H, O): the service wave's, or (kInline) each wave's
   const int H = p.nodes[1];
   const int b = p.bias;
   const int wave = threadIdx.x >> 6;
   const int lane64 = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < kSlots; i += kSvcThreads) lds_st(&slots[i].flag, 0);
+  for (int i = threadIdx.x; i < kSlots; i += kSvcThreads) {
+    lds_st(&slots[i].flag, 0);
+    slots[i].rec = 0;
+  }
   const bool tabbed = p.n_games <= kServeTabSlots;
   if (tabbed)
     for (int i = threadIdx.x; i < p.n_games * kServeTabPoints; i += kSvcThreads)
@@ -124,7 +181,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   }
   __syncthreads();
 
-  if (wave == kSvcGameWaves) {
+  if (!kInline && wave == kSvcGameWaves) {
     // ---------------- service wave: f64 re-decisions for the whole block ----
     // the service wave's issue priority over its SIMD partner (a game wave):
     // an answer sooner is a requester's wait shorter (PG_SVC_PRIO 3 vs 0,
@@ -228,7 +285,15 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   const int leader = lane64 & ~(L - 1);
   // index (not a pointer) into the __shared__ array keeps every mailbox access
   // a ds_* instruction; a SlowSlot * decays to a flat pointer
-  const int sx = (threadIdx.x / L) * 2 + side;
+  // The group's mailbox slots, recomputed from the lane id where a rare block
+  // uses them (v_mbcnt in volatile asm, not hoisted): as loop-invariant lane
+  // values they were spilled and reloaded from scratch in those blocks.
+  const int wave_slot0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * (64 / L) * 2;
+  const auto slot_grp = [&]() { return wave_slot0 + (fresh_lane64() / L) * 2; };  // the group's side-0 slot
+  const auto slot_me = [&]() {  // this half's slot
+    const int l = fresh_lane64();
+    return wave_slot0 + (l / L) * 2 + ((l & (L - 1)) >= HL ? 1 : 0);
+  };
   const WT *genomes = (const WT *)p.genomes;
   const WT *opponents = (const WT *)p.opponents;
 
@@ -240,7 +305,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   // plain frame updates neither; total (main.py:73) and the score-based end
   // (main.py:102-107) change only at a point, inside the rare block
   // act_r / act_l: the actions written into action[4:6] / [6:8] (main.py:91-92)
-  // as 8 x code (code 0 = [0,0], 1 = up, 2 = down), the next step's table offset
+  // as the paddles' moves in centroid units (clamp_move: -6 up, +6 down, 0), which the step adds
   // c_vis: the game's visible frames (a forward each), counted per frame --
   // or, kVisByFrames, the frame counter at its start: an instance that
   // advances every hidden serve delay at once steps exactly one hidden frame
@@ -263,11 +328,29 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     w = group_broadcast<L>(ww, leader);
   }
   bool fresh = true;
-  bool w_scripted = true, w_onep = true;  // wave-uniform; set at the first frame's starts
+  // kInline: every lane stays in the loop until its wave has no game left
+  // (serve_inline needs the whole wave); a group without work is parked as a
+  // ball at rest mid-field, visible (vis = 2: no decision, no face, no point)
+  // and never timed out, and the wave leaves when none of its groups is live
+  bool live = w < games_total;
+  const auto park = [&]() {
+    st.bx2 = 2 * 79 + kBallW - 1;
+    st.by2 = 2 * 78 + kBallH - 1;
+    st.vx2 = st.vy2 = 0;
+    st.vis = 2;
+    st.one_player = 0;
+    kind = kOppNN;
+    tend = 0x7fffffff;
+    fresh = false;
+  };
+  if (kInline && !live) park();
+  // wave-uniform (kept as scalars: readfirstlane, so no lane mask is rebuilt
+  // from a vector copy every frame); set at the first frame's starts
+  int w_scripted = 1, w_onep = 1;
   // wave-uniform: some game of the wave starts, or has a hidden ball whose serve
   // delay the top block advances; set where that can change (the top block, the
   // rare block), so a plain frame tests one scalar
-  bool top = true;
+  int top = 1;
 #ifdef PG_PROBE_EXTRA
   float probe_v = 0.f;
   float2v probe_p = float2v{0.f, 0.f};
@@ -288,8 +371,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #else
 #define PG_PP(cnt, cond)
 #endif
-  // a group leaves the loop at its game-end block when the queue is empty (no per-frame test)
-  if (w < games_total) for (;;) {
+  // a group leaves the loop at its game-end block when the queue is empty (no
+  // per-frame test); kInline: the wave, when its last live group has ended
+  if (kInline ? __builtin_amdgcn_ballot_w64(live) != 0 : live) for (;;) {
 #ifdef PG_START_PROBE
     const bool any_fresh = __builtin_amdgcn_ballot_w64(fresh) != 0;
     const uint64_t probe_f0 = __builtin_amdgcn_s_memtime();
@@ -314,7 +398,10 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       const bool nn = side && kind == kOppNN && p.n_opponents > 0;
       const int oj = nn ? min(max(p.opp[w], 0), p.n_opponents - 1) : 0;
       gm = nn ? opponents + (long)oj * p.ostride : gr;
-      load_rec<U, O>(net, p.recs + ((nn ? (long)p.n_genomes + oj : (long)i) * HL + hl) * rec_floats<U, O>());
+      const int rec = nn ? p.n_genomes + oj : i;
+      load_rec<U, O>(net, p.recs + ((long)rec * HL + hl) * rec_floats<U, O>());
+      const int sx = slot_me();
+      if (kInline && hl == 0) slots[sx].rec = rec;
       // the output bias enters the first lane's two partial chains, half each
       // (exact), so the frame adds no bias after the group sum (partial_pk)
 #pragma unroll
@@ -360,8 +447,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         st.rc2 = PongK::drift2(st.rc2, h);
         if (!st.one_player) st.lc2 = PongK::drift2(st.lc2, h);
         st.timer = 1;
-        act_r = clamp_action8(st.rc2, 0);
-        act_l = clamp_action8(st.lc2, 0);  // (a 1-player env's CPU paddle: unclipped, the same side of the band)
+        act_r = clamp_move(st.rc2, 0);
+        act_l = clamp_move(st.lc2, 0);  // (a 1-player env's CPU paddle: unclipped, the same side of the band)
         fstart -= h;  // frames += h, and the no-score counter with them
         tend -= h;
         hidden += h;
@@ -370,9 +457,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #endif
     // the wave's games after any start: is one of them scripted, or a
     // 1-player env (both fixed for a game; no per-frame test otherwise)
-    w_scripted = PG_ANY(kind != kOppNN);
-    w_onep = PG_ANY(st.one_player != 0);
-    top = false;  // every start and serve delay above is done
+    w_scripted = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(kind != kOppNN) != 0);
+    w_onep = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(st.one_player != 0) != 0);
+    top = 0;  // every start and serve delay above is done
     }
     const int pvis = st.vis, pbx2 = st.bx2, pby2 = st.by2;
 #ifdef PG_PATH_PROBE
@@ -380,7 +467,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #endif
     const int ev = st.step(act_r, act_l, [&](int pt) {
       return tabbed && pt < kServeTabPoints ? serve_tab[tab_off + pt] : Pong::serve_entry(st.seed, pt);
-    }, w_onep);
+    }, w_onep != 0);
     PG_PP(pp_face, ev != kStepFly || st.hits != hits_b || st.point != pt_b);
     const int vis = st.vis;
     const int bx2 = st.bx2, by2 = st.by2;
@@ -408,25 +495,85 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       pg_probe_extra<PG_PROBE_EXTRA>(net.w1[0][0], net.w1[1][1], z[0], z[1], probe_v, probe_p, probe_s);
 #endif
       const bool left_nn = kind == kOppNN;
-      if (side && !left_nn) code = 8;  // the left half is idle against a scripted opponent
-      if (!vis) code = 0;
+      if (side && !left_nn) code = 0;  // the left half is idle against a scripted opponent
+      if (vis != 1) code = 0;  // the ball hidden ([0,0]) or a parked group
 #ifdef PG_ABLATE_SLOW  // timing-only build: never re-decide in f64
-      if (code < 0) code = z[1] > z[0] ? 16 : 8;
+      if (code == -1) code = z[1] > z[0] ? 6 : -6;
 #endif
-      PG_PP(pp_fail, code < 0);
+      PG_PP(pp_fail, code == -1);
       // rare, half-uniform: the in-wave plateau rule, then the memo, else ask
       // the service wave (one wave-uniform test on the common path)
-      if (PG_ANY(code < 0)) {
-      if (code < 0) {
+      if (PG_ANY(code == -1)) {
+      if (code == -1) {
         fails += 1;
 #ifdef PG_TIMELINE
         g_fails += 1;
 #endif
         const int idx = plateau_f32<O>(z, net.e);
         inwave += idx >= 0 ? 1 : 0;
-        code = idx >= 0 ? index_to_code8(idx) : -1;
+        code = idx >= 0 ? index_to_move(idx) : -1;
       }
-      if (PG_ANY(code < 0) && code < 0) {
+      if (kInline && PG_ANY(code == -1)) {
+        // the memo, then the whole wave decides each still-undecided half-group in turn
+        uint64_t key = 0;
+        int nm = 0;
+        const int sx = slot_me();
+        if (code == -1) {
+          key = memo_key(k);
+          nm = slots[sx].n_memo;
+          int hit = -1;
+#pragma unroll 1
+          for (int c = 0; c < kMemo && c < nm; ++c)
+            if (slots[sx].memo_key[c] == key) hit = slots[sx].memo_idx[c];
+          code = hit;
+        }
+        // the request: the network's own features (x-flipped for the left paddle), its f32 outputs and bound
+        const int kn[6] = {side ? 320 - bx2 : bx2, by2, side ? 320 - lbx2 : lbx2, lby2, side ? lc2 : rc2,
+                           side ? rc2 : lc2};
+        const float my_e = net.e;
+        uint64_t need = __builtin_amdgcn_ballot_w64(code == -1 && hl == 0);
+        if (need) {
+        if constexpr (PG_INLINE_PRIO > 0) __builtin_amdgcn_s_setprio(PG_INLINE_PRIO);
+#pragma unroll 1
+        do {
+          const int src = (int)__builtin_ctzll(need);
+          need &= need - 1;
+          InlineReq r;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) r.k[i] = __builtin_amdgcn_readlane(kn[i], src);
+#pragma unroll
+          for (int o = O; o < 4; ++o) r.z[o] = 0.f;
+#pragma unroll
+          for (int o = 0; o < O; ++o) r.z[o] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z[o]), src));
+          r.e = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_e), src));
+          const uint64_t ga = (uint64_t)gm;
+          const WT *g = (const WT *)(((uint64_t)__builtin_amdgcn_readlane((int)(ga >> 32), src) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ga, src));
+          const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64);
+          if ((lane64 & ~(HL - 1)) == src) {  // the requesting half-group
+            slow += (ans >> 8) & 1;
+            plateau += ans >> 9;
+            code = index_to_move(ans & 255);
+            if (hl == 0) {
+              const int c = nm % kMemo;  // round-robin replacement
+              slots[sx].memo_key[c] = key;
+              slots[sx].memo_idx[c] = code;
+              slots[sx].n_memo = nm + 1;
+            }
+          }
+        } while (need);
+        if constexpr (PG_INLINE_PRIO > 0) __builtin_amdgcn_s_setprio(0);
+        {
+          // the networks back from their lane records: nothing of the game
+          // loop's weights stays live across serve_inline's calls
+          load_rec<U, O>(net, p.recs + ((long)slots[sx].rec * HL + hl) * rec_floats<U, O>());
+#pragma unroll
+          for (int o = 0; o < O; ++o) net.c[o] = hl == 0 ? 0.5f * net.c[o] : 0.f;
+        }
+        }
+      }
+      if (!kInline && PG_ANY(code == -1) && code == -1) {
+        const int sx = slot_me();
         const uint64_t key = memo_key(k);
         const int nm = slots[sx].n_memo;
         int hit = -1;
@@ -458,7 +605,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           g_slow += 1;  // service round trips
 #endif
           plateau += ans >> 9;
-          code = index_to_code8(ans & 255);
+          code = index_to_move(ans & 255);
           if (hl == 0) {
             const int c = nm % kMemo;  // round-robin replacement
             slots[sx].memo_key[c] = key;
@@ -476,18 +623,18 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       // HardcodedAi / ScoreHardcodedAi (dumb_ais.py): behind a wave-uniform
       // test, which a self-play schedule never passes
       if (__builtin_expect(w_scripted, 0) && !left_nn) {
-        left = vis ? hardcoded8(by2, lc2) : 0;
+        left = vis ? hardcoded_move(by2, lc2) : 0;
         if (kind == kOppScore && st.s1 > st.s2) left = 0;
       }
       if constexpr (!kVisByFrames) c_vis += vis;  // forwards: c_vis x (1 or 2 networks), counted at the game's end
     }
-    act_l = clamp_action8(lc2, left);
-    act_r = clamp_action8(rc2, right);
+    act_l = clamp_move(lc2, left);
+    act_r = clamp_move(rc2, right);
 #ifndef PG_TIMELINE
     if (!kUntraced && p.trace) {  // a wave-uniform test first: untraced launches skip the per-lane ones
       const int frames = sframe - fstart;
-      if (w < p.trace_games && frames <= p.trace_cap && lig == 0)
-        p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)((act_r >> 3) | ((act_l >> 3) << 2) | (vis << 4));
+      if (w < p.trace_games && frames <= p.trace_cap && lig == 0 && (!kInline || live))
+        p.trace[(long)w * p.trace_cap + frames - 1] = (uint8_t)(move_code(act_r) | (move_code(act_l) << 2) | (vis << 4));
     }
 #endif
     // calculate_timeout_and_frames (main.py:128-135); at most one point a frame
@@ -528,13 +675,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       total += sframe - 1 - (tend - kTimeoutThresh);
       tend = sframe + kTimeoutThresh;
       over = over || st.s1 >= kWinScore || st.s2 >= kWinScore || st.done();
-      if (lig == 0) slots[(threadIdx.x / L) * 2].rally_at = -1;  // the next rally searches afresh
+      if (lig == 0) slots[slot_grp()].rally_at = -1;  // the next rally searches afresh
     }
 #ifndef PG_NO_RALLY_SKIP
     const int timeout = sframe - (tend - kTimeoutThresh);
     if (rally_check && timeout <= kTimeoutThresh) {
-      const int rs = (threadIdx.x / L) * 2;  // the group's side-0 slot
-      const uint64_t key = st.key(act_r >> 3, act_l >> 3);
+      const int rs = slot_grp();  // the group's side-0 slot
+      const uint64_t key = st.key(move_code(act_r), move_code(act_l));
       const int at = slots[rs].rally_at;
       if (at > timeout || at < 0) {
         if (lig == 0) {
@@ -615,11 +762,23 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       int ww = 0;
       if (lig == 0) ww = (int)atomicAdd(p.work, 1u);
       w = group_broadcast<L>(ww, leader);
-      if (w >= games_total) break;
-      fresh = true;
+      if constexpr (kInline) {
+        if (w >= games_total) {
+          live = false;
+          park();
+        } else {
+          fresh = true;
+        }
+      } else {
+        if (w >= games_total) break;
+        fresh = true;
+      }
+    }
+    if constexpr (kInline) {
+      if (__builtin_amdgcn_ballot_w64(live) == 0) break;
     }
     // what the next frame's top block has to do: a start, or (a point) a serve delay to advance
-    top = PG_ANY(fresh || (kJumps && !st.vis && st.timer >= 2));
+    top = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(fresh || (kJumps && !st.vis && st.timer >= 2)) != 0);
     }
   }
   if (p.counters && c_games) {
@@ -671,8 +830,11 @@ inline size_t service_records_bytes(int n_genomes, int n_opponents, int L, int U
 template <int L, int U, int O, typename WT, bool kSplitTrace = false>
 inline int32_t launch_service(const EvalParams &p, hipStream_t s) {
   constexpr int kSvcThreads = svc_threads<U>();
-  constexpr int GPB = (kSvcThreads / 64 - 1) * (64 / L);  // game groups per block
-  const size_t lds = (size_t)f64_lds_doubles(p.nodes[1], O) * sizeof(double);
+  // game groups per block, and the f64 scratch: the service wave's, or each wave's
+  // (the horizon instance keeps the service wave: inline_service<L, U, true>)
+  const bool inl = p.horizon > 0 ? inline_service<L, U, true>() : inline_service<L, U, false>();
+  const int GPB = (kSvcThreads / 64 - (inl ? 0 : 1)) * (64 / L);
+  const size_t lds = (size_t)f64_lds_doubles(p.nodes[1], O) * sizeof(double) * (inl ? kSvcThreads / 64 : 1);
   const int want = (p.total + GPB - 1) / GPB;
   const int cap = num_cus() * 2;
   const int grid = want < cap ? want : cap;
