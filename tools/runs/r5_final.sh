@@ -1,4 +1,5 @@
-# round 5, the final library (one call): the whole -m gpu suite and smoke();
+# round 5, the final library (one call; its -m gpu suite ran in call b8 on
+# the same library, profiles/r05/lib_sha_b8.txt): smoke();
 # the FETCH_SIZE / WRITE_SIZE PMC passes of every bench workload (reduced by
 # tools/pmc_traffic.py, hash-matched to the library) copied into this box's
 # profiles/r05/ so that the bench lines after them report roofline.traffic;
@@ -11,7 +12,6 @@ export TMPDIR=/tmp
 TAG=${RUN:-r5_final}
 OUT=gpurun_out/$TAG; mkdir -p $OUT; ROOT=$(pwd)
 sha256sum neuro-genetic-pong-self-play_amd/libpong_ga.so > $OUT/lib_sha.txt
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || exit 1
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1
 pmc() {  # tag, kernel, output name, bench args...
   local tag=$1 kern=$2 name=$3; shift 3
