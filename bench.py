@@ -171,7 +171,7 @@ def main():
     steps_local = 0
     fwd_local = 0
     slow_local = 0
-    cert_local = [0, 0, 0]  # certificate failures, decided by the service wave, decided in-wave
+    cert_local = [0, 0, 0]  # certificate failures, decided by the f64 certificate, decided by the f32 plateau rule
     passes_local = 0        # k_wide: network weight passes (each streams one network's genes once)
     skip_local = 0          # episode frames of periodic rallies advanced at once (counters[8])
     hidden_local = 0        # serve-delay frames advanced at once (counters[12])
@@ -286,7 +286,7 @@ def main():
                        "serve_delay_frames_advanced_per_generation": hidden_all / args.steps,
                        "certificate_failures_per_forward": cert_all[0] / max(fwd_all, 1.0),
                        "failures_decided_in_wave": cert_all[2] / max(cert_all[0], 1.0),
-                       "failures_decided_by_service_f64_certificate": cert_all[1] / max(cert_all[0], 1.0),
+                       "failures_decided_by_f64_certificate": cert_all[1] / max(cert_all[0], 1.0),
                        "numpy_order_f64_forwards_per_forward": slow_all / max(fwd_all, 1.0)},
             "roofline": _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_per_forward,
                                            fwd_per_launch, steps_per_launch, streaming_bytes, n_local, H),
@@ -338,7 +338,7 @@ def _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_pe
                       "instructions per env-step are physics, features, certificate and bookkeeping, not the "
                       "network's FMAs (DESIGN.md 4.1; SQ counters: profiles/%s/sq_summary_final.txt)" % PROFILE_ROUND,
             "kernel": "k_service<8,16,3,double> (pg_eval_population: 8 games per wave, 4 lanes per network, "
-                      "f64 service wave per block)",
+                      "8 game waves per block; certificate failures decided by the wave itself)",
             "kernel_ms_per_launch": kernel_ms_mean,
             "flops_per_forward": flops_per_forward,
             "forwards_per_launch": fwd_per_launch,
