@@ -176,12 +176,16 @@ struct NetP {
   Cert ct;           // certify_c's constants from e (load_rec)
 };
 
-// Number of f32 roundings in one output sum of the packed forward: a chain of
-// P pk_fma per component, the .x + .y fold, the group tree, + c, and the
-// f32 rounding of W2 -- bounded by U + log2(HL) + 3 for every layout.
+// Number of f32 roundings one term of an output sum of the packed forward
+// passes: the chain of P = (U + 1) / 2 pk_fma of its component (partial_pk:
+// unit 2p + h lands in component h), the .x + .y fold, the log2(HL) levels of
+// the group tree, the + c after it (or, partial_pk's kBiasIn, nothing: the
+// bias shares start the chains), and the f32 rounding of W2: P + log2(HL) + 3.
+// (Until round 5 the bound took U for P, twice the chain: a wider bound, more
+// certificate failures, the same decisions.)
 template <int HL, int U>
 __host__ __device__ constexpr int out_roundings() {
-  return U + (HL >= 32 ? 5 : HL >= 16 ? 4 : HL >= 8 ? 3 : HL >= 4 ? 2 : HL >= 2 ? 1 : 0) + 3;
+  return (U + 1) / 2 + (HL >= 32 ? 5 : HL >= 16 ? 4 : HL >= 8 ? 3 : HL >= 4 ? 2 : HL >= 2 ? 1 : 0) + 3;
 }
 
 // flip (the left paddle's network in k_service): the x-flip and me/enemy
@@ -300,6 +304,36 @@ __device__ __forceinline__ void store_rec(const NetP<U, O> &n, float *__restrict
   float4 *d = reinterpret_cast<float4 *>(r);
 #pragma unroll
   for (int q = 0; q < F / 4; ++q) d[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+// The output layer's part of a lane record (w2 pairs, c, e; after the P x 7
+// w1 pairs): what k_service's in-wave decision path hands to the f64 code's
+// registers and reloads afterwards (the record's 16-B pieces from the one
+// holding the first w2 float).
+template <int U, int O>
+__device__ __forceinline__ void load_rec_out(NetP<U, O> &n, const float *__restrict__ r) {
+  constexpr int P = NetP<U, O>::P;
+  constexpr int F = rec_floats<U, O>();
+  constexpr int B = P * 14 / 4 * 4;  // the 16-B piece holding the first w2 float
+  constexpr int D = P * 14 - B;       // (0 when P is even)
+  const float4 *s = reinterpret_cast<const float4 *>(r + B);
+  float v[F - B];
+#pragma unroll
+  for (int q = 0; q < (F - B) / 4; ++q) {
+    const float4 x = s[q];
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int o = 0; o < O; ++o) n.w2[p][o] = float2v{v[D + (p * O + o) * 2], v[D + (p * O + o) * 2 + 1]};
+#pragma unroll
+  for (int o = 0; o < O; ++o) n.c[o] = v[D + P * O * 2 + o];
+  n.e = v[D + P * O * 2 + O];
+  n.ct = make_cert(n.e);
 }
 
 template <int U, int O>

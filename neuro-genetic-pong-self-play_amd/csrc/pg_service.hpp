@@ -566,7 +566,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         {
           // the networks back from their lane records: nothing of the game
           // loop's weights stays live across serve_inline's calls
-          load_rec<U, O>(net, p.recs + ((long)slots[sx].rec * HL + hl) * rec_floats<U, O>());
+          load_rec_out<U, O>(net, p.recs + ((long)slots[sx].rec * HL + hl) * rec_floats<U, O>());
 #pragma unroll
           for (int o = 0; o < O; ++o) net.c[o] = hl == 0 ? 0.5f * net.c[o] : 0.f;
         }
