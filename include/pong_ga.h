@@ -100,8 +100,9 @@ typedef enum pg_kernel {
   PG_KERNEL_AUTO = 0,      /* SPLIT when the shape and precision allow, else GENERAL */
   PG_KERNEL_GENERAL = 1,   /* one wave per game, f64, any NETWORK_SHAPE */
   PG_KERNEL_RESIDENT = 2,  /* retired (round 4): PG_ERR_UNSUPPORTED */
-  PG_KERNEL_SPLIT = 3      /* [6, H<=256, 2..4]: half a lane group per paddle's network, plus one
-                              f64 service wave per 1024-thread block for re-decisions */,
+  PG_KERNEL_SPLIT = 3      /* [6, H<=256, 2..4]: half a lane group per paddle's network; f32 forwards with
+                              a certified argmax, the failures re-decided in f64 by the wave itself
+                              (8-lane groups) or by one service wave per block (other layouts) */,
   PG_KERNEL_WIDE = 4,      /* [6, H1<=512, H2<=512, 1..4]: one 512-thread workgroup per genome plays its
                               games (up to 6; more: balanced chunks of <= 6, one workgroup pass each)
                               in lockstep and streams W2 from HBM each frame
@@ -158,8 +159,8 @@ typedef struct pg_eval_args {
   int32_t *status;               /* [n_genomes] 1 = ZeroDivisionError in calculate_reward */
   uint64_t *counters;            /* optional [16], zeroed by the call: [0] env steps stepped one frame at a time, [1] NN
                                     forwards, [2] numpy-order f64 forwards, [3] games; split kernel: [4]
-                                    f32 certificate failures, [5] failures decided by the service wave's
-                                    certified f64 rules, [6] failures decided in-wave by the f32 plateau
+                                    f32 certificate failures, [5] failures decided by the certified f64
+                                    rules (plateau, gap), [6] failures decided in-wave by the f32 plateau
                                     rule; wide kernel: [7] network weight passes; split and wide
                                     kernels: [8] episode frames of periodic rallies advanced to their
                                     timeout at once; [9] hard decisions (see hard_log); split kernel:
@@ -173,8 +174,8 @@ typedef struct pg_eval_args {
   void *workspace;               /* device scratch of pg_eval_workspace_bytes() bytes */
   size_t workspace_bytes;
   uint32_t *hard_log;            /* optional [hard_cap][8] records of the decisions no bound settles
-                                    (fixtures for tests/golden/nn_hard_cases): split kernel, forwards its
-                                    service wave hands to the numpy-order f64 forward; wide kernel,
+                                    (fixtures for tests/golden/nn_hard_cases): split kernel, forwards the
+                                    certified f64 rules hand to the numpy-order f64 forward; wide kernel,
                                     decisions whose two largest activations lie within 1e-12 (not both
                                     1.0).  Record: {row, flags, k0..k5}; flags bit 0 = row of the
                                     opponents (else genomes), bits 8..15 the decided index, bits 16..23
@@ -227,7 +228,7 @@ typedef struct pg_forward_args {
  * genome_index[i] (i if NULL) on the doubled-centroid features k[i][0..5]
  * (utils.inference's inputs are k / 320; main.py:143-150).  It runs the very
  * cascade k_service runs in a game -- the f32 pass and its certificate, the
- * in-wave plateau rule, the service wave's plateau and certified f64 rules,
+ * in-wave plateau rule, the f64 plateau and certified rules,
  * and last the numpy-order f64 forward -- so fixtures of hard inputs pin the
  * hot kernel's decisions.  [6, H <= 256, 2..4] networks. */
 typedef struct pg_decide_args {
@@ -239,7 +240,7 @@ typedef struct pg_decide_args {
   const int32_t *k;              /* [n, 6] doubled centroids, each in [0, 320] */
   int32_t *index;                /* out [n] np.argmax of NeuralNetwork.run's activations */
   int32_t *stage;                /* optional out [n]: 0 f32 certificate, 1 in-wave plateau rule,
-                                    2 service wave's certified rules, 3 numpy-order f64 forward */
+                                    2 certified f64 rules, 3 numpy-order f64 forward */
 } pg_decide_args;
 
 /* The wide kernel's decision for given inputs: k_wide itself (the evaluation

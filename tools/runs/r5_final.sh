@@ -1,5 +1,6 @@
-# round 5, the final library (one call; its -m gpu suite ran in call b8 on
-# the same library, profiles/r05/lib_sha_b8.txt): smoke();
+# round 5, the final library (one call; its -m gpu suite ran in the call
+# before it on the same library -- b8 for a095280e, b9 for the next --
+# profiles/r05/lib_sha_b*.txt): smoke();
 # the FETCH_SIZE / WRITE_SIZE PMC passes of every bench workload (reduced by
 # tools/pmc_traffic.py, hash-matched to the library) copied into this box's
 # profiles/r05/ so that the bench lines after them report roofline.traffic;
