@@ -501,8 +501,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       if (code == -1) code = z[1] > z[0] ? 6 : -6;
 #endif
       PG_PP(pp_fail, code == -1);
-      // rare, half-uniform: the in-wave plateau rule, then the memo, else ask
-      // the service wave (one wave-uniform test on the common path)
+      // rare, half-uniform: the in-wave plateau rule, then the memo, else the
+      // f64 stage -- the whole wave (kInline) or the service wave (one
+      // wave-uniform test on the common path)
       if (PG_ANY(code == -1)) {
       if (code == -1) {
         fails += 1;

@@ -8,8 +8,9 @@
 //
 //   k_service<L,U,O,WT>   [6, H<=256, O] networks (pg_service.hpp): an aligned
 //                         group of L lanes plays one game, half a group per
-//                         paddle's network in VGPRs, one f64 service wave per
-//                         block; f32 math with a certified f64 argmax.
+//                         paddle's network in VGPRs; f32 math with a certified
+//                         f64 argmax, the failures re-decided in f64 by the
+//                         wave itself (8-lane groups) or a service wave.
 //   k_general<WT>         any NETWORK_SHAPE, one wave per game, f64 numpy_nn
 //                         arithmetic with activations staged in LDS.
 //   k_fitness             sum(all_rewards) / GAMES_TO_PLAY in the reference order.
