@@ -360,6 +360,10 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
   uint64_t probe_fresh = 0;
   const uint64_t probe_t0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef PG_DECIDE_PROBE  // diagnostic build: shader cycles of kInline's f64 decisions (until the reload has landed) vs the wave's total
+  uint64_t probe_dec = 0;
+  const uint64_t probe_t0 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef PG_TIMELINE
   uint64_t t_start = 0;
   uint32_t g_fails = 0, g_slow = 0;
@@ -534,6 +538,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         const float my_e = net.e;
         uint64_t need = __builtin_amdgcn_ballot_w64(code == -1 && hl == 0);
         if (need) {
+#ifdef PG_DECIDE_PROBE
+        const uint64_t probe_d0 = __builtin_amdgcn_s_memtime();
+#endif
         if constexpr (PG_INLINE_PRIO > 0) __builtin_amdgcn_s_setprio(PG_INLINE_PRIO);
 #pragma unroll 1
         do {
@@ -565,11 +572,15 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         } while (need);
         if constexpr (PG_INLINE_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         {
-          // the networks back from their lane records: nothing of the game
-          // loop's weights stays live across serve_inline's calls
+          // the output layer back from the lane records: its registers were
+          // the f64 code's (the input layer's stay live across it)
           load_rec_out<U, O>(net, p.recs + ((long)slots[sx].rec * HL + hl) * rec_floats<U, O>());
 #pragma unroll
           for (int o = 0; o < O; ++o) net.c[o] = hl == 0 ? 0.5f * net.c[o] : 0.f;
+#ifdef PG_DECIDE_PROBE
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          probe_dec += __builtin_amdgcn_s_memtime() - probe_d0;
+#endif
         }
         }
       }
@@ -797,6 +808,13 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     if (hl == 0 && plateau) atomicAdd((unsigned long long *)&p.counters[5], (unsigned long long)plateau);
     if (hl == 0 && inwave) atomicAdd((unsigned long long *)&p.counters[6], (unsigned long long)inwave);
   }
+#ifdef PG_DECIDE_PROBE
+  if (p.counters && lane64 == 0) {
+    atomicAdd((unsigned long long *)&p.counters[13], (unsigned long long)probe_dec);
+    atomicAdd((unsigned long long *)&p.counters[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - probe_t0));
+    atomicAdd((unsigned long long *)&p.counters[15], 1ull);
+  }
+#endif
 #ifdef PG_START_PROBE
   if (p.counters && lane64 == 0) {
     atomicAdd((unsigned long long *)&p.counters[13], (unsigned long long)probe_fresh);
