@@ -882,6 +882,22 @@ __device__ int f64_decide_sums(const double *zp, const double *ep, const double 
     mhi[o] = __builtin_amdgcn_readlane(m, 2 * o);
     mlo[o] = __builtin_amdgcn_readlane(m, 2 * o + 1);
   }
+  // the plateau width above each output's top, lane w for output w: one
+  // exp per lane instead of one per (w, o) pair of the test below (their
+  // registers spilled on this path)
+  double tw[O];
+  {
+    double top = z[0] + e[0];
+#pragma unroll
+    for (int o = 1; o < O; ++o)
+      if (lane == o) top = z[o] + e[o];
+    const double twl = 8.881784197001252e-16 * (pg_exp_f64(fmin(top, 40.0)) + 1.0);
+    const uint64_t tb = (uint64_t)__double_as_longlong(twl);
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+      tw[o] = __longlong_as_double((long long)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(tb >> 32), o) << 32) |
+                                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tb, o)));
+  }
 #pragma unroll
   for (int w = 0; w < O; ++w) {
     bool ok = true;
@@ -890,11 +906,9 @@ __device__ int f64_decide_sums(const double *zp, const double *ep, const double 
       if (o == w) continue;
       if (mhi[w] != kBig) {  // w surely in the plateau regime
         ok = ok && (o < w ? mhi[w] < mlo[o] : mhi[w] <= mlo[o]);
-      } else {  // S_w below the regime: a strict gap above the plateau width
-        const double top = z[w] + e[w];
-        const double tw = 8.881784197001252e-16 * (pg_exp_f64(fmin(top, 40.0)) + 1.0);
+      } else {  // S_w below the regime: a strict gap above the plateau width tw[w]
         // and S_w normal (z > -1022 ln 2; S = 0.0 for all z < -709.78, see certify)
-        ok = ok && (z[w] - e[w] > z[o] + e[o] + tw) && (z[w] - e[w] > -708.0);
+        ok = ok && (z[w] - e[w] > z[o] + e[o] + tw[w]) && (z[w] - e[w] > -708.0);
       }
     }
     if (ok) return w;
