@@ -409,6 +409,69 @@ __device__ __forceinline__ void partial_pk(const NetP<U, O> &n, const int k[6], 
   for (int o = 0; o < O; ++o) acc[o] = a2[o].x + a2[o].y;
 }
 
+// The bound of one frame (serve_inline, before the f64 stage): load_net_pk's
+// derivation with this frame's magnitudes where it takes the worst case.  Per
+// hidden unit j, in a' = -a log2 e units (the records'):
+//   R'_j  = sum_i |w'_ji k_i| + |w'_j6|  (+ 2^-20 320 sum_i |w'_ji|, the
+//           x-flip fold's f64 rounding)       instead of |x_i| <= 1
+//   da'_j = 11u R'_j                            the pre-activation error
+//   slope = min(1/4, 2^(2 da'_j - |a'_j|))      s(1-s) <= e^-|a| = 2^-|a'|, over
+//           every point within 2 da'_j of the recomputed a'_j (the true one
+//           and partial_pk's: both within da'_j of the exact value)
+//                                               instead of 1/4
+//   ds_j  = slope da'_j ln 2 + 5u s_j + 2^-100  the sigmoid's error: the
+//           propagated part and v_exp/+1/v_rcp's relative ~1 ulp each (s = 0
+//           or 1 saturated: the floor)          instead of 3u R_j + 5u
+//   z_o error <= sum_j |W2_oj| (ds_j + OR u s_j) + OR u |c_o|
+//           (OR = out_roundings, its terms' magnitudes |W2_oj s_j|)
+// and twice the largest over o, as load_net_pk.  Saturated units -- most of
+// an evolved network's -- drop out of the propagated part and negative ones
+// out of the sums', so the frame's bound is ~4x tighter than the network's on
+// the bench's N(0, 3) genes (tests/test_frame_bound.py restates it in numpy
+// and checks it against f64): the near-ties it separates skip the f64 stage.
+// By the whole wave for one half-group's network: lane t takes the units of
+// slot t (rec: the half-group's first lane record; record hl holds units
+// hl + HL u, u = 2p + h, and the full output biases), so the requesting
+// lanes' registers are not needed -- they are the f64 code's by then.
+template <int HL, int U, int O>
+__device__ __forceinline__ float frame_bound_wave(const float *__restrict__ rec, const int k[6], int lane64) {
+  constexpr int P = NetP<U, O>::P;
+  constexpr int F = rec_floats<U, O>();
+  constexpr float kOR = (float)out_roundings<HL, U>();
+  float acc[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) acc[o] = 0.f;
+#pragma unroll 1
+  for (int t = lane64; t < HL * 2 * P; t += 64) {  // padding units hold zero weights
+    const int hl = t % HL, u = t / HL, p = u >> 1, h = u & 1;
+    const float *r = rec + hl * F;
+    float w[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w[i] = r[(p * 7 + i) * 2 + h];
+    float w2[O];
+#pragma unroll
+    for (int o = 0; o < O; ++o) w2[o] = r[P * 14 + (p * O + o) * 2 + h];
+    float a = w[6], rr = fabsf(w[6]), ws = fabsf(w[6]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      a = fmaf(w[i], (float)k[i], a);
+      rr = fmaf(fabsf(w[i]), (float)k[i], rr);
+      ws += fabsf(w[i]);
+    }
+    const float da = (rr + ws * (320.f * 9.5367431640625e-7f)) * (11.f * kU);
+    const float sl = fminf(0.25f, __builtin_amdgcn_exp2f(2.f * da - fabsf(a)));
+    const float s = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(a) + 1.0f);
+    const float ds = sl * da * 0.6931471805599453f + s * ((5.f + kOR) * kU) + 7.8886090522101181e-31f;
+#pragma unroll
+    for (int o = 0; o < O; ++o) acc[o] = fmaf(fabsf(w2[o]), ds, acc[o]);
+  }
+  float e = 0.f;
+#pragma unroll
+  for (int o = 0; o < O; ++o)
+    e = fmaxf(e, 2.f * (group_sum<64>(acc[o]) + kOR * kU * fabsf(rec[P * 14 + P * O * 2 + o])));
+  return e;
+}
+
 // Certified argmax of S(z) = 1/(1 + pow(e, -z)) in f64 (numpy_nn.py:22-23,131)
 // given |z_true - z[o]| <= e.  S is exactly 1.0 iff z >= 53 ln 2 =
 // 36.73680056967710 (then every saturated output ties and the first wins);

@@ -50,15 +50,17 @@ __host__ __device__ constexpr bool inline_service() {
 }
 
 // One request, by the whole wave (every lane active): the f32 outputs'
-// plateau rule, else the certified f64 decision, else numpy's own order in
-// f64 (lds: this wave's f64_lds_doubles(H, O) scratch).  The answer as the
-// service wave's: the index, bit 8 numpy-order, bit 9 certified.  Not
-// inlined: its registers are the callee's, saved around the call on this
-// rare path, not added to the game loop's budget.
+// plateau rule, then the two f32 rules again under the frame's own bound
+// (frame_bound_wave, from the network's lane records), else the certified f64
+// decision, else numpy's own order in f64 (lds: this wave's
+// f64_lds_doubles(H, O) scratch).  The answer: the index, bit 8 numpy-order,
+// bit 9 certified in f64, bit 10 certified by the frame's bound.
 struct InlineReq {
-  int k[6];
+  int k[6];    // the network's own features (x-flipped for the left paddle): the genes' f64 forward
+  int kr[6];   // the game's features as the records take them (the flip is in the weights)
   float z[4];
   float e;
+  const float *rec;  // the half-group's first lane record
 };
 template <int U, int HL, int O, typename WT>
 __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, InlineReq r, double *lds,
@@ -69,6 +71,13 @@ __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, In
 #pragma unroll
   for (int o = 0; o < O; ++o) zf[o] = r.z[o];
   int d = plateau_decide<O>(zf, r.e, lane64);
+  if (d < 0 && r.e < __builtin_inff()) {  // e = inf: weights over the cap, f64 only
+    const float ef = fminf(r.e, frame_bound_wave<HL, U, O>(r.rec, r.kr, lane64));
+    d = certify_c<O>(zf, make_cert(ef));
+    if (d < 0) d = plateau_f32<O>(zf, ef);
+    if (d < 0) d = plateau_decide<O>(zf, ef, lane64);
+    if (d >= 0) return d | 1024;
+  }
   if (d < 0) d = fast_f64_decide<O, WT>(g, H, b, r.k, lane64);
   if (d >= 0) return d | 512;
   d = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, r.k, lds, lane64);
@@ -550,6 +559,9 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #pragma unroll
           for (int i = 0; i < 6; ++i) r.k[i] = __builtin_amdgcn_readlane(kn[i], src);
 #pragma unroll
+          for (int i = 0; i < 6; ++i) r.kr[i] = __builtin_amdgcn_readlane(k[i], src);
+          r.rec = p.recs + (long)__builtin_amdgcn_readlane(slots[sx].rec, src) * HL * rec_floats<U, O>();
+#pragma unroll
           for (int o = O; o < 4; ++o) r.z[o] = 0.f;
 #pragma unroll
           for (int o = 0; o < O; ++o) r.z[o] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z[o]), src));
@@ -560,7 +572,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64);
           if ((lane64 & ~(HL - 1)) == src) {  // the requesting half-group
             slow += (ans >> 8) & 1;
-            plateau += ans >> 9;
+            plateau += (ans >> 9) & 1;
+            inwave += ans >> 10;
             code = index_to_move(ans & 255);
             if (hl == 0) {
               const int c = nm % kMemo;  // round-robin replacement
