@@ -1,7 +1,7 @@
 # round 5, call b12: the frame's own error bound (frame_bound) before the f64
 # stage -- load_net_pk's derivation with the frame's magnitudes, ~4x tighter
 # than the network's static bound on N(0,3) networks: the whole -m gpu suite,
-# then same-box A/Bs against the shipped library (0a51d667 as ab/lib_0a51.so)
+# then same-box A/Bs against the library before it (0a51d667 as ab/lib_0a51.so)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${RUN:-r5_b12}; mkdir -p $OUT

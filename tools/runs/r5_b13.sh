@@ -2,7 +2,7 @@
 # (frame_bound_wave, from the lane records; b12 computed it in the requesting
 # lanes and spilled: 1.08 vs 1.20 ·10^10), ahead of the f64 genome fetch:
 # the whole -m gpu suite,
-# then same-box A/Bs against the shipped library (0a51d667 as ab/lib_0a51.so)
+# then same-box A/Bs against the library before it (0a51d667 as ab/lib_0a51.so)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${RUN:-r5_b13}; mkdir -p $OUT
