@@ -240,7 +240,9 @@ typedef struct pg_decide_args {
   const int32_t *k;              /* [n, 6] doubled centroids, each in [0, 320] */
   int32_t *index;                /* out [n] np.argmax of NeuralNetwork.run's activations */
   int32_t *stage;                /* optional out [n]: 0 f32 certificate, 1 in-wave plateau rule,
-                                    2 certified f64 rules, 3 numpy-order f64 forward */
+                                    2 certified f64 rules, 3 numpy-order f64 forward,
+                                    4 the f32 rules under the frame's own bound (H in 33..64,
+                                    the layout whose k_service decides in the game wave) */
 } pg_decide_args;
 
 /* The wide kernel's decision for given inputs: k_wide itself (the evaluation

@@ -184,10 +184,12 @@ __global__ __launch_bounds__(64) void k_general(EvalParams p) {
 // k_service's decision cascade on given inputs (pg_decide): the split layout's
 // f32 pass (load_net_pk / partial_pk / group_sum<HL>, the same z and bound e a
 // game half-group computes), certify, the in-wave plateau rule, then the
-// service wave's plateau_decide, fast_f64_decide and numpy-order forward --
-// the same device functions, so a fixture of hard inputs pins the decisions
-// k_service makes on them.  One wave: 64 / HL passes' f32 parts in parallel,
-// then each failing pass through the wave-wide service cascade.
+// service wave's plateau_decide, the frame's own bound where k_service uses it
+// (serve_inline's layout: frame_bound_wave over the passes' lane records, kept
+// in LDS here), fast_f64_decide and numpy-order forward -- the same device
+// functions, so a fixture of hard inputs pins the decisions k_service makes on
+// them.  One wave: 64 / HL passes' f32 parts in parallel, then each failing
+// pass through the wave-wide service cascade.
 struct DecideParams {
   const void *genomes;
   const int32_t *gidx;
@@ -201,6 +203,9 @@ struct DecideParams {
 template <int HL, int U, int O, typename WT>
 __global__ __launch_bounds__(64) void k_decide(DecideParams p) {
   constexpr int GPW = 64 / HL;
+  constexpr bool kFrameBound = inline_service<2 * HL, U, false>();
+  constexpr int F = rec_floats<U, O>();
+  __shared__ float recs_dec[kFrameBound ? 64 * F : 1];  // lane t's record at t * F
   extern __shared__ double lds_dec[];  // f64_lds_doubles(H, O)
   __shared__ float zs[GPW][4];
   __shared__ float es[GPW];
@@ -213,6 +218,7 @@ __global__ __launch_bounds__(64) void k_decide(DecideParams p) {
       const WT *g = genomes + (long)(p.gidx ? p.gidx[t] : t) * p.gstride;
       NetP<U, O> net;
       load_net_pk<HL, U, O, WT>(net, g, p.H, p.b, hl);
+      if constexpr (kFrameBound) store_rec<U, O>(net, recs_dec + lane * F);
       int k[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) k[i] = p.k[(long)t * 6 + i];
@@ -246,6 +252,15 @@ __global__ __launch_bounds__(64) void k_decide(DecideParams p) {
       for (int o = 0; o < O; ++o) zf[o] = zs[q][o];
       int idx = plateau_decide<O>(zf, es[q], lane);
       int st = 2;
+      if constexpr (kFrameBound) {
+        if (idx < 0 && es[q] < __builtin_inff()) {  // serve_inline's order
+          const float ef = fminf(es[q], frame_bound_wave<HL, U, O>(recs_dec + q * HL * F, k, lane));
+          idx = certify_c<O>(zf, make_cert(ef));
+          if (idx < 0) idx = plateau_f32<O>(zf, ef);
+          if (idx < 0) idx = plateau_decide<O>(zf, ef, lane);
+          st = idx >= 0 ? 4 : 2;
+        }
+      }
       if (idx < 0) idx = fast_f64_decide<O, WT>(g, p.H, p.b, k, lane);
       if (idx < 0) {
         idx = forward_f64_group<64, 1, O, WT>(g, p.H, p.b, (const int *)k, lds_dec, lane);

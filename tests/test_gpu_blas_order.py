@@ -80,14 +80,14 @@ def test_f64_layers_in_numpy_order(gpu, oracle, tmp_path, shape, bias, n_gen):
 
 @pytest.mark.parametrize("shape", [[6, 64, 3], [6, 2, 2], [6, 16, 4], [6, 100, 3], [6, 200, 2]])
 def test_decide_cascade_equals_f64(gpu, shape):
-    """pg_decide (k_service's cascade: f32 certificate, plateau rules, certified
-    f64, numpy-order f64) == the all-f64 forward's argmax on 300k+ decisions,
+    """pg_decide (k_service's cascade: f32 certificate, plateau rules, the
+    frame's own bound, certified f64, numpy-order f64) == the all-f64 forward's argmax on 300k+ decisions,
     incl. the saturation-heavy N(0, 9) / N(0, 30) regimes."""
     from pong_amd.device import Evaluator
     rng = np.random.default_rng(shape[1] * 7 + shape[2])
     G = _gene_count(shape)
     ev = Evaluator(shape, device=gpu)
-    stages = np.zeros(4, np.int64)
+    stages = np.zeros(5, np.int64)
     for sigma in (1.0, 3.0, 9.0, 30.0):
         n_gen, per = 512, 160
         genes = torch.tensor(rng.standard_normal((n_gen, G)) * sigma, device=gpu)
@@ -97,6 +97,9 @@ def test_decide_cascade_equals_f64(gpu, shape):
         x = torch.tensor(k * 0.5 / 160.0, device=gpu)
         ref, _ = ev.forward(genes, x, genome_index=gi, precision="f64", want_act=False)
         np.testing.assert_array_equal(idx.cpu().numpy(), ref.cpu().numpy())
-        stages += np.bincount(stage.cpu().numpy(), minlength=4)
-    print(f"shape {shape}: decision stages {stages.tolist()} (f32, in-wave plateau, service certified, numpy-order)")
+        stages += np.bincount(stage.cpu().numpy(), minlength=5)
+    print(f"shape {shape}: decision stages {stages.tolist()} (f32, in-wave plateau, service certified, numpy-order, "
+          "frame bound)")
     assert stages[0] > 0.9 * stages.sum()
+    if shape[1] > 32 and shape[1] <= 64:  # serve_inline's layout (L = 8, U = 16): the frame bound's tier runs
+        assert stages[4] > 0

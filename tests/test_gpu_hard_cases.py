@@ -22,9 +22,11 @@ def test_split_hard_cases_decide_as_numpy(gpu):
     g = torch.tensor(c["genes"], device=gpu)
     idx, stage = ev.decide(g, torch.tensor(c["k"], device=gpu))
     np.testing.assert_array_equal(idx.cpu().numpy(), c["idx_ref"])
-    st = np.bincount(stage.cpu().numpy(), minlength=4)
+    st = np.bincount(stage.cpu().numpy(), minlength=5)
     print(f"{len(c['idx_ref'])} hard cases, stages {st.tolist()}")
-    assert st[3] > 0.9 * st.sum()  # they are the numpy-order forward's cases
+    # they are the numpy-order forward's cases (the frame's own bound, stage 4,
+    # may settle a plateau tie among them first)
+    assert st[3] + st[4] > 0.9 * st.sum()
     i64, act = ev.forward(g, torch.tensor(c["x"], device=gpu), precision="f64")
     np.testing.assert_array_equal(i64.cpu().numpy(), c["idx_ref"])
     np.testing.assert_allclose(act.cpu().numpy(), c["act_ref"], rtol=0, atol=1e-12)
