@@ -279,7 +279,10 @@ class Evaluator:
     # --------------------------------------------------------------- decide
     def decide(self, genomes: torch.Tensor, k: torch.Tensor, genome_index: Optional[torch.Tensor] = None):
         """The split kernel's decision cascade (pg_decide) on doubled-centroid
-        features k [n, 6] int32: returns (argmax index [n] int32, stage [n] int32)."""
+        features k [n, 6] int32: returns (argmax index [n] int32, stage [n] int32):
+        0 f32 certificate, 1 in-wave plateau rule, 2 certified f64 rules,
+        3 numpy-order f64 forward, 4 the f32 rules under the frame's own bound
+        (pg_decide_args.stage)."""
         dev = self.device
         _need(genomes, "genomes", self.dtype, dev)
         n = k.shape[0]
