@@ -12,9 +12,10 @@ random features, that
     (numpy_nn.py:120-137's z), with the bound's x2 margin untouched, and
   * the frame bound never exceeds the static one (the kernel takes the min),
     and is several times tighter for the bench's sigma = 3 networks.
-numpy's f32 exp2 and division are correctly rounded, v_exp_f32 / v_rcp_f32
-are within ~1 ulp; the bound budgets 5u relative for the sigmoid's three
-roundings, so the emulation sits inside the hardware's error model.
+numpy's f32 division is correctly rounded and its exp2 within an ulp, as
+v_exp_f32 / v_rcp_f32 are within ~1 ulp; the bound budgets 5u relative for
+the sigmoid's three roundings, so the emulation sits inside the hardware's
+error model.
 """
 import numpy as np
 import pytest
