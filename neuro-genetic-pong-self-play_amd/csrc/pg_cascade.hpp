@@ -6,8 +6,8 @@
 //   partial_f32 / partial_pk the hidden layer and lane-partial output sums
 //   certify                  argmax of numpy's f64 S(z) proven from f32 z +- e
 //   plateau_f32              the same near saturation, in-wave
-//   plateau_decide / fast_f64_decide / forward_f64_group
-//                            the service wave's f64 steps (numpy_nn.py:120-137)
+//   plateau_decide / frame_bound_wave / fast_f64_decide / forward_f64_group
+//                            the f64 stage and its f32 frame bound (numpy_nn.py:120-137)
 // DESIGN.md 4.1 "Certified argmax, as a cascade".
 #pragma once
 
