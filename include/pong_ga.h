@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 10
+#define PG_ABI_VERSION 11
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -131,7 +131,7 @@ typedef struct pg_net {
 } pg_net;
 
 typedef struct pg_eval_args {
-  /* ABI 10: sizeof(pg_eval_args) as the caller compiled it.  pg_eval_population
+  /* ABI 10 (11: + timeout_thresh, win_score): sizeof(pg_eval_args) as the caller compiled it.  pg_eval_population
    * and pg_eval_workspace_bytes refuse any other value (PG_ERR_INVALID / 0
    * bytes): a binding whose struct is shorter or longer than this header's
    * would otherwise have the library read past it.  Always the first field,
@@ -202,6 +202,13 @@ typedef struct pg_eval_args {
                                     the sum of the completed episodes' rewards in order, scores = the points
                                     of all its episodes (score1, score2), frames = T, total_frames = the
                                     completed episodes, status = any ZeroDivisionError; fitness as usual. */
+  /* ABI 11: the episode limits of perform_episode (main.py:102-107), config.py's TIMEOUT_THRESH
+     and WIN_SCORE; 0 = the reference's values (2000, 3).  A game ends when a score reaches
+     win_score (1..21; the env's own end at 21 comes first above that) or when the no-score
+     counter of calculate_timeout_and_frames (main.py:128-135) exceeds timeout_thresh
+     (32..1048576: never while a served ball is still hidden, 30 frames). */
+  int32_t timeout_thresh;
+  int32_t win_score;
 } pg_eval_args;
 
 /* Trace byte: right_code | left_code << 2 | ball_visible << 4, where a code is

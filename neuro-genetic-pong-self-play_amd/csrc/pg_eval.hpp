@@ -48,6 +48,8 @@ struct EvalParams {
   int n_nodes, bias, max_width;
   float *recs;         // split kernel: lane records (k_prep_records), [n_genomes + n_opponents][L/2][rec_floats]
   int horizon;         // pg_eval_args.horizon: fixed-horizon measurement mode (T frames per game slot), 0 = off
+  int timeout_thresh;  // pg_eval_args.timeout_thresh: TIMEOUT_THRESH (kTimeoutThresh unless set)
+  int win_score;       // pg_eval_args.win_score: WIN_SCORE (kWinScore unless set)
   int prep;            // pg_prep: which records k_prep_records writes; it also zeroes the work header and
                        // the counters when its launch precedes the games (PG_PREP_ALL / PG_PREP_REST)
   void *wide_scratch;  // k_wide: the blocks' tile-major W2 copies (workspace)

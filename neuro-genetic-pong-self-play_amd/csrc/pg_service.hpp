@@ -428,7 +428,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       act_r = act_l = total = 0;
       c_vis = kVisByFrames ? sframe - 1 : 0;
       fstart = sframe - 1;             // this iteration is the game's frame 1
-      tend = sframe + kTimeoutThresh;  // frame 1 does not count (main.py:94-96): it takes the counter to 0
+      tend = sframe + p.timeout_thresh;  // frame 1 does not count (main.py:94-96): it takes the counter to 0
       fresh = false;
       if (hl == 0) slots[sx].n_memo = 0;
       if (lig == 0) slots[sx].rally_at = -1;  // (sx is the side-0 slot there)
@@ -697,14 +697,18 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     // check is off, tracing: one compare on the common path instead of three)
     if (PG_ANY((kHorizon ? !same : ev >= kStepPoint) || over)) {
     if (!same) {  // a point: total_frames += timeout, timeout = 0 (main.py:128-135); the scores' end test
-      total += sframe - 1 - (tend - kTimeoutThresh);
-      tend = sframe + kTimeoutThresh;
-      over = over || st.s1 >= kWinScore || st.s2 >= kWinScore || st.done();
+      total += sframe - 1 - (tend - p.timeout_thresh);
+      tend = sframe + p.timeout_thresh;
+      // the counter is reset before the termination test (main.py:94-107): a
+      // point on the frame the counter would pass TIMEOUT_THRESH ends the game
+      // only by the scores (round-5 review: `over` kept the pre-point timeout)
+      over = st.s1 >= p.win_score || st.s2 >= p.win_score || st.done();
+      if constexpr (kHorizon) over = over || sframe - fstart >= p.horizon;
       if (lig == 0) slots[slot_grp()].rally_at = -1;  // the next rally searches afresh
     }
 #ifndef PG_NO_RALLY_SKIP
-    const int timeout = sframe - (tend - kTimeoutThresh);
-    if (rally_check && timeout <= kTimeoutThresh) {
+    const int timeout = sframe - (tend - p.timeout_thresh);
+    if (rally_check && timeout <= p.timeout_thresh) {
       const int rs = slot_grp();  // the group's side-0 slot
       const uint64_t key = st.key(move_code(act_r), move_code(act_l));
       const int at = slots[rs].rally_at;
@@ -715,7 +719,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           slots[rs].rally_span = kRallySpan0;
         }
       } else if (slots[rs].rally_key == key) {
-        const int rest = kTimeoutThresh + 1 - timeout;
+        const int rest = p.timeout_thresh + 1 - timeout;
         fstart -= rest;  // frames += rest; the counter at TIMEOUT_THRESH + 1
         skipped += rest;
         tend = sframe - 1;
@@ -732,7 +736,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     if constexpr (kHorizon) {
       if (over) {  // an episode's end or the horizon's
         const int gx = threadIdx.x / L;
-        const bool ep_end = st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || sframe > tend;
+        const bool ep_end = st.s1 >= p.win_score || st.s2 >= p.win_score || st.done() || sframe > tend;
         if (lig == 0) {
           if (ep_end) {  // perform_episode's reward (main.py:108-112), summed in episode order
             int zd;
@@ -748,7 +752,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           st.reset(st.seed, st.one_player);
           st.point = pt;
           act_r = act_l = total = 0;
-          tend = sframe + 1 + kTimeoutThresh;  // the next iteration is the episode's frame 1
+          tend = sframe + 1 + p.timeout_thresh;  // the next iteration is the episode's frame 1
           over = false;
         }
       }

@@ -808,7 +808,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
 #ifndef PG_NO_RALLY_SKIP
           // a periodic rally ends at the timeout with nothing else changed (pg_device.hpp
           // rally_key); no state of a point recurs before its kRallyHits-th return
-          if (st.hits >= kRallyHits && g.timeout <= kTimeoutThresh && (g.timeout & (kRallyStride - 1)) == 0 &&
+          if (st.hits >= kRallyHits && g.timeout <= p.timeout_thresh && (g.timeout & (kRallyStride - 1)) == 0 &&
               !p.trace) {
             const uint64_t key = rally_key(st, g.act_r, g.act_l);
             if (rat[lane] < 0) {
@@ -816,10 +816,10 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
               rat[lane] = g.timeout;
               rspan[lane] = kRallySpan0;
             } else if (rkey[lane] == key) {
-              const int rest = kTimeoutThresh + 1 - g.timeout;
+              const int rest = p.timeout_thresh + 1 - g.timeout;
               g.frames += rest;
               cnt[lane * 4 + 3] += rest;
-              g.timeout = kTimeoutThresh + 1;
+              g.timeout = p.timeout_thresh + 1;
             } else if (g.timeout - rat[lane] >= rspan[lane]) {
               rkey[lane] = key;
               rat[lane] = g.timeout;
@@ -827,7 +827,7 @@ __global__ __launch_bounds__(kWideThreads) void k_wide(EvalParams p) {
             }
           }
 #endif
-          if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || g.timeout > kTimeoutThresh) {
+          if (st.s1 >= p.win_score || st.s2 >= p.win_score || st.done() || g.timeout > p.timeout_thresh) {
             finish_game(p, w, st, g.frames, g.total);
             g.active = 0;
             cnt[lane * 4 + 0] += g.frames;

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(64) void k_general(EvalParams p) {
           timeout = 0;
         }
       }
-      if (st.s1 >= kWinScore || st.s2 >= kWinScore || st.done() || timeout > kTimeoutThresh) break;
+      if (st.s1 >= p.win_score || st.s2 >= p.win_score || st.done() || timeout > p.timeout_thresh) break;
     }
     c_steps += frames;
     c_games += 1;
@@ -222,10 +222,15 @@ __global__ __launch_bounds__(64) void k_decide(DecideParams p) {
       int k[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) k[i] = p.k[(long)t * 6 + i];
-      float acc[O], z[O];
-      partial_pk<U, O>(net, k, acc);
+      // k_service's order: the output bias enters the first lane's two partial
+      // chains, half each (exact), no add after the group sum -- the same f32 z
+      // bit for bit (round-5 review: this pass had kept the bias after the sum)
 #pragma unroll
-      for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]) + net.c[o];
+      for (int o = 0; o < O; ++o) net.c[o] = hl == 0 ? 0.5f * net.c[o] : 0.f;
+      float acc[O], z[O];
+      partial_pk<U, O, true>(net, k, acc);
+#pragma unroll
+      for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]);
       int idx = certify<O>(z, net.e), st = 0;
       if (idx < 0) {
         idx = plateau_f32<O>(z, net.e);
@@ -860,6 +865,9 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
   if (a->n_genomes < 0) return fail(PG_ERR_INVALID, "n_genomes=%d < 0", a->n_genomes);
   if (a->n_games < 1 || a->n_games > 64) return fail(PG_ERR_INVALID, "n_games=%d not in [1, 64]", a->n_games);
   if (a->horizon < 0) return fail(PG_ERR_INVALID, "horizon=%d < 0", a->horizon);
+  if (a->timeout_thresh != 0 && (a->timeout_thresh < 32 || a->timeout_thresh > (1 << 20)))
+    return fail(PG_ERR_INVALID, "timeout_thresh=%d not 0 or in [32, 1048576]", a->timeout_thresh);
+  if (a->win_score < 0) return fail(PG_ERR_INVALID, "win_score=%d < 0", a->win_score);
   if (a->n_genomes == 0) {  // nothing to play (e.g. an empty shard); the counters still read zero
     if (a->counters) PG_HIP(hipMemsetAsync(a->counters, 0, 16 * sizeof(uint64_t), (hipStream_t)stream));
     return PG_OK;
@@ -922,6 +930,9 @@ int32_t pg_eval_population(const pg_eval_args *a, void *stream) {
 
   p.prep = a->prep;
   p.horizon = a->horizon;
+  p.timeout_thresh = a->timeout_thresh > 0 ? a->timeout_thresh : kTimeoutThresh;
+  // above the env's own end (a score of 21, Pong::done) WIN_SCORE changes nothing
+  p.win_score = a->win_score > 0 ? (a->win_score < kDoneScore ? a->win_score : kDoneScore) : kWinScore;
   const int kernel = resolve_kernel(a);
   if (kernel != PG_KERNEL_SPLIT) {
     if (a->prep == PG_PREP_GENOMES) return PG_OK;  // no records outside the split kernel

@@ -30,7 +30,7 @@ from utils import pick_hall_of_famer, save_checkpoint
 def _evaluator():
     # the network shape is utils' binding, as create_model_from_genes sees it (utils.py:80-87)
     return runtime.evaluator(utils.NETWORK_SHAPE, utils.BIAS, GAMES_TO_PLAY, GENOME_DTYPE,  # noqa: F405
-                             PRECISION, PHYSICS_SEED, DEVICE)  # noqa: F405
+                             PRECISION, PHYSICS_SEED, DEVICE, TIMEOUT_THRESH, WIN_SCORE)  # noqa: F405
 
 
 def _fitness_tuples(fitness, status):
@@ -155,7 +155,7 @@ def perform_episode(env, left_model, right_model, render=False, score_multiplier
     else:
         raise TypeError(f"left_model {type(left_model).__name__} has no device game kind")
     ev = runtime.evaluator(right_model.nodes, bool(right_model.bias), 1, "float64", PRECISION,  # noqa: F405
-                           _slot_seed(getattr(env, "game", 0)), DEVICE)  # noqa: F405
+                           _slot_seed(getattr(env, "game", 0)), DEVICE, TIMEOUT_THRESH, WIN_SCORE)  # noqa: F405
     dev = ev.device
     kind_t = torch.tensor([[kind]], dtype=torch.int32, device=dev)
     opp_t = torch.zeros((1, 1), dtype=torch.int32, device=dev)

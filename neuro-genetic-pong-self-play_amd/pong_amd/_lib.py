@@ -16,7 +16,7 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 10
+PG_ABI_VERSION = 11
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -41,7 +41,7 @@ class PgNet(ctypes.Structure):
 
 class PgEvalArgs(ctypes.Structure):
     _fields_ = [
-        ("struct_size", ctypes.c_uint32),  # ABI 10: sizeof(pg_eval_args); the library refuses any other value
+        ("struct_size", ctypes.c_uint32),  # ABI 10+: sizeof(pg_eval_args); the library refuses any other value
         ("net", PgNet),
         ("n_genomes", ctypes.c_int32), ("n_games", ctypes.c_int32),
         ("genomes", _vp), ("genome_stride", ctypes.c_int64),
@@ -57,6 +57,7 @@ class PgEvalArgs(ctypes.Structure):
         ("hard_log", _vp), ("hard_cap", ctypes.c_int32), ("genome_rows", _vp),
         ("n_active", _vp),
         ("prep", ctypes.c_int32), ("horizon", ctypes.c_int32),
+        ("timeout_thresh", ctypes.c_int32), ("win_score", ctypes.c_int32),  # ABI 11
     ]
 
     def __init__(self, *args, **kw):

@@ -38,17 +38,64 @@ def _obj(name: str) -> str:
     return os.path.join(CSRC, name + ".o")
 
 
-def _stale(obj: str, src: str) -> bool:
-    """An object is rebuilt when it is missing or older than its source, any
-    shared header or this file (headers are not tracked per unit)."""
-    if not os.path.exists(obj):
+def _flags() -> list:
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off"] + [
+        # no SLP packing of independent f32 adds into v_pk_add_f32: it breaks the
+        # DPP-fused reductions into mov_dpp + pk_add pairs (measured -5 %)
+        "-fno-slp-vectorize", "-fPIC",
+        "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO_DIR, "include")]
+
+
+def _unit_cmd(src: str, extra: list, out: str) -> list:
+    return [HIPCC] + _flags() + SOURCE_FLAGS.get(os.path.basename(src), []) + extra + ["-c", "-o", out, src]
+
+
+def _link_cmd(objs: list, out: str) -> list:
+    return [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", out] + sorted(objs)
+
+
+def _read(path: str):
+    try:
+        with open(path) as fh:
+            return fh.read()
+    except OSError:
+        return None
+
+
+def _write(path: str, text: str) -> None:
+    with open(path + ".tmp", "w") as fh:
+        fh.write(text)
+    os.replace(path + ".tmp", path)
+
+
+# Stamps: each object's compile command and the library's whole recipe (every
+# unit's command and the link's), written next to them.  A build input that is
+# not a file -- PG_OFFLOAD_ARCH, HIPCC, the flags above -- changes the command,
+# so an object or library built with another one is rebuilt, not linked into a
+# library labelled with the new arch (round-5 review).
+def _unit_stamp(name: str, src: str, extra: list) -> str:
+    return " ".join(_unit_cmd(os.path.join(CSRC, src), extra, _obj(name)))
+
+
+def _lib_stamp() -> str:
+    lines = [_unit_stamp(name, src, extra) for name, src, extra in sorted(UNITS)]
+    lines.append(" ".join(_link_cmd([_obj(name) for name, _, _ in UNITS], LIB_PATH)))
+    return "\n".join(lines) + "\n"
+
+
+def _stale(name: str, src: str, extra: list) -> bool:
+    """An object is rebuilt when it is missing, older than its source, any
+    shared header or this file (headers are not tracked per unit), or was
+    compiled by another command."""
+    obj = _obj(name)
+    if not os.path.exists(obj) or _read(obj + ".stamp") != _unit_stamp(name, src, extra):
         return True
     t = os.path.getmtime(obj)
-    return any(os.path.getmtime(d) > t for d in [src, os.path.abspath(__file__)] + HEADERS)
+    return any(os.path.getmtime(d) > t for d in [os.path.join(CSRC, src), os.path.abspath(__file__)] + HEADERS)
 
 
 def needs_build() -> bool:
-    if not os.path.exists(LIB_PATH):
+    if not os.path.exists(LIB_PATH) or _read(LIB_PATH + ".stamp") != _lib_stamp():
         return True
     t = os.path.getmtime(LIB_PATH)
     return any(os.path.getmtime(d) > t for d in DEPS)
@@ -59,32 +106,28 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB_PATH  # a prebuilt variant (tools/build_variant.py): never rebuilt from the product sources
     if not force and not needs_build():
         return LIB_PATH
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off"] + [
-             # no SLP packing of independent f32 adds into v_pk_add_f32: it breaks the
-             # DPP-fused reductions into mov_dpp + pk_add pairs (measured -5 %)
-             "-fno-slp-vectorize", "-fPIC",
-             "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO_DIR, "include")]
     objs, procs = [], []
     # the slow units first, so the parallel build ends sooner
     for name, src, extra in sorted(UNITS, key=lambda u: not u[0].startswith("pg_service_more")):
-        src = os.path.join(CSRC, src)
         obj = _obj(name)
         objs.append(obj)
-        if not force and not _stale(obj, src):
+        if not force and not _stale(name, src, extra):
             continue
-        cmd = [HIPCC] + flags + SOURCE_FLAGS.get(os.path.basename(src), []) + extra + ["-c", "-o", obj + ".tmp", src]
+        cmd = _unit_cmd(os.path.join(CSRC, src), extra, obj + ".tmp")
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        procs.append((subprocess.Popen(cmd), cmd, obj))
-    for proc, cmd, obj in procs:
+        procs.append((subprocess.Popen(cmd), cmd, obj, _unit_stamp(name, src, extra)))
+    for proc, cmd, obj, stamp in procs:
         if proc.wait() != 0:
             raise subprocess.CalledProcessError(proc.returncode, cmd)
         os.replace(obj + ".tmp", obj)
-    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", LIB_PATH + ".tmp"] + sorted(objs)
+        _write(obj + ".stamp", stamp)
+    link = _link_cmd(objs, LIB_PATH + ".tmp")
     if verbose:
         print(" ".join(link), file=sys.stderr)
     subprocess.check_call(link)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    _write(LIB_PATH + ".stamp", _lib_stamp())
     return LIB_PATH
 
 

@@ -78,7 +78,8 @@ class Evaluator:
     """Population evaluator for one NETWORK_SHAPE on one device."""
 
     def __init__(self, nodes, bias=True, dtype=torch.float64, device=None, n_games=6,
-                 precision="certified", kernel="auto", group_lanes=0, seed=0, horizon=0):
+                 precision="certified", kernel="auto", group_lanes=0, seed=0, horizon=0,
+                 timeout_thresh=0, win_score=0):
         if not torch.cuda.is_available():
             raise RuntimeError("pong_amd.Evaluator needs a HIP device (no CPU fallback)")
         L.lib()
@@ -94,6 +95,10 @@ class Evaluator:
         # pg_eval_args.horizon: 0 = evaluate()'s episodes; T > 0 = SURVEY 8(d)'s
         # fixed-horizon measurement mode (T frames per game slot, auto-reset)
         self.horizon = int(horizon)
+        # pg_eval_args.timeout_thresh / win_score: config.py's TIMEOUT_THRESH and
+        # WIN_SCORE (perform_episode's termination, main.py:102-107); 0 = 2000 / 3
+        self.timeout_thresh = int(timeout_thresh)
+        self.win_score = int(win_score)
         self.genes = gene_count(self.nodes, self.bias)
         self.net = L.make_net(self.nodes, self.bias, DTYPES[dtype])
         self._ws = None
@@ -218,6 +223,7 @@ class Evaluator:
             raise ValueError("prep='rest' needs a preceding prep='genomes' call with the same genomes, rows, "
                              "n_active and row count on this evaluator")
         a.horizon = self.horizon if horizon is None else int(horizon)
+        a.timeout_thresh, a.win_score = self.timeout_thresh, self.win_score
         a.kernel = KERNELS[kernel or self.kernel]
         a.group_lanes = self.group_lanes if group_lanes is None else int(group_lanes)
         ws = self._workspace(a)

@@ -58,7 +58,7 @@ class DeviceGA:
                  n_games: int = 6, schedule: str = "reference", cxpb: float = 0.9, mutpb: float = 0.9,
                  alpha: float = 0.9, mu: float = 0.0, sigma: float = 0.9, indpb: float = 0.9,
                  seed: int = 0, physics_seed: int = 0, precision: str = "certified", kernel: str = "auto",
-                 group=None, hof_block_rows: int = 0):
+                 group=None, hof_block_rows: int = 0, timeout_thresh: int = 0, win_score: int = 0):
         if schedule not in D.SCHEDULES:
             raise ValueError(f"schedule must be one of {sorted(D.SCHEDULES)}")
         self.nodes = [int(v) for v in nodes]
@@ -69,7 +69,8 @@ class DeviceGA:
         if self.P < 1 or self.H < 0 or self.tournsize < 1:
             raise ValueError("population_size >= 1, hof_size >= 0 and tournsize >= 1 required")
         self.ev = D.Evaluator(self.nodes, bias=bias, dtype=dtype, device=device, n_games=n_games,
-                              precision=precision, kernel=kernel, seed=physics_seed)
+                              precision=precision, kernel=kernel, seed=physics_seed,
+                              timeout_thresh=timeout_thresh, win_score=win_score)
         self.device, self.dtype, self.G = self.ev.device, dtype, self.ev.genes
         self.bias, self.n_games, self.schedule = bool(bias), int(n_games), schedule
         self.cxpb, self.mutpb, self.alpha = float(cxpb), float(mutpb), float(alpha)
@@ -91,8 +92,10 @@ class DeviceGA:
         if self.hof_block_rows > 0 and schedule == "selfplay":
             self.hof_slices = max(1, min(-(-self.P // self.hof_block_rows), max(self.H, 1)))
         B = self.hof_block_rows
-        self._slice = (self.lo // B if self.hof_slices > 1 and self.hi > self.lo and self.lo // B == (self.hi - 1) // B
-                       else None)
+        # the slice k_schedule gives this block: (row // B) mod K (round-5 review:
+        # without the mod a block index >= K named a slice the schedule never plays)
+        self._slice = ((self.lo // B) % self.hof_slices
+                       if self.hof_slices > 1 and self.hi > self.lo and self.lo // B == (self.hi - 1) // B else None)
         self.store = torch.zeros((self.H + self.P, self.G), dtype=dtype, device=self.device)
         self.spare = torch.empty_like(self.store)
         self.fitness = torch.zeros(self.P, dtype=torch.float64, device=self.device)

@@ -18,8 +18,9 @@ def _torch_dtype(name: str):
 
 
 def evaluator(nodes, bias=True, n_games=6, genome_dtype="float64", precision="certified",
-              seed=0, device="cuda") -> D.Evaluator:
-    key = (tuple(int(n) for n in nodes), bool(bias), int(n_games), genome_dtype, precision, int(seed), str(device))
+              seed=0, device="cuda", timeout_thresh=0, win_score=0) -> D.Evaluator:
+    key = (tuple(int(n) for n in nodes), bool(bias), int(n_games), genome_dtype, precision, int(seed), str(device),
+           int(timeout_thresh), int(win_score))
     with _lock:
         ev = _evaluators.get(key)
         if ev is None:
@@ -27,7 +28,8 @@ def evaluator(nodes, bias=True, n_games=6, genome_dtype="float64", precision="ce
             if dev.type == "cuda" and dev.index is None:
                 dev = torch.device("cuda", torch.cuda.current_device())
             ev = D.Evaluator(list(nodes), bias=bias, dtype=_torch_dtype(genome_dtype), device=dev,
-                             n_games=n_games, precision=precision, seed=seed)
+                             n_games=n_games, precision=precision, seed=seed,
+                             timeout_thresh=timeout_thresh, win_score=win_score)
             _evaluators[key] = ev
         return ev
 

@@ -185,8 +185,12 @@ class _Env:
         return self.frame, 0.0, bool(self.L.or_env_done(ctypes.byref(s))), {"score1": s.score1, "score2": s.score2}
 
 
-def perform_episode(env, left_model, right_model, score_multiplier):
-    """main.py:69-112.  Returns (reward, frames, score1, score2, total_frames)."""
+def perform_episode(env, left_model, right_model, score_multiplier, timeout_thresh=None, win_score=None):
+    """main.py:69-112.  Returns (reward, frames, score1, score2, total_frames).
+    ``timeout_thresh`` / ``win_score``: config.py's TIMEOUT_THRESH / WIN_SCORE
+    (None: the reference's 2000 / 3)."""
+    thresh = TIMEOUT_THRESH if not timeout_thresh else timeout_thresh
+    win = WIN_SCORE if not win_score else win_score
     last_score = None
     action = _blank_action()
     timeout_counter = 0.0
@@ -210,11 +214,11 @@ def perform_episode(env, left_model, right_model, score_multiplier):
                 total_frames += timeout_counter
                 timeout_counter = 0.0
         last_score = score_info
-        if score_info["score1"] >= WIN_SCORE or score_info["score2"] >= WIN_SCORE:
+        if score_info["score1"] >= win or score_info["score2"] >= win:
             break
         if is_done:
             break
-        if timeout_counter > TIMEOUT_THRESH:
+        if timeout_counter > thresh:
             break
     s1, s2 = score_info["score1"], score_info["score2"]
     if s1 == s2:
@@ -224,7 +228,7 @@ def perform_episode(env, left_model, right_model, score_multiplier):
     return reward, frames, s1, s2, total_frames
 
 
-def evaluate(nodes, genes, kinds, opp_rows, mults, opponents, base_seed=0):
+def evaluate(nodes, genes, kinds, opp_rows, mults, opponents, base_seed=0, timeout_thresh=None, win_score=None):
     """main.py:28-66 for one genome with a fixed game schedule (kind 0 HardcodedAi,
     1 ROM CPU, 2 ScoreHardcodedAi, 3 network opponent ``opponents[opp_rows[g]]``
     with ``right_score_multiplier = mults[g]``).  Returns (fitness, rewards, frames)."""
@@ -235,7 +239,8 @@ def evaluate(nodes, genes, kinds, opp_rows, mults, opponents, base_seed=0):
         left = (NumpyNet(nodes, opponents[int(opp_rows[g])]) if k == 3
                 else ScoreHardcoded() if k == 2 else Hardcoded())
         env = _Env(O.game_seed(base_seed, g), k == 1)
-        rew, f, _s1, _s2, _tf = perform_episode(env, left, right, float(mults[g]) if k == 3 else 1.0)
+        rew, f, _s1, _s2, _tf = perform_episode(env, left, right, float(mults[g]) if k == 3 else 1.0,
+                                                timeout_thresh, win_score)
         rewards.append(rew)
         frames += f
     return sum(rewards) / float(GAMES_TO_PLAY), rewards, frames

@@ -91,6 +91,8 @@ def lib() -> ctypes.CDLL:
         u8p = ctypes.POINTER(ctypes.c_uint8)
         L.or_render.argtypes = [ctypes.POINTER(OrState), u8p]
         L.or_find_stuff.argtypes = [u8p, dp]
+        L.or_set_limits.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.or_set_limits.restype = None
         _lib = L
     return _lib
 
@@ -171,9 +173,32 @@ class Env:
         return {name: getattr(self.state, name) for name, _ in OrState._fields_}
 
 
-def play_game(genes, nodes, opp_kind, opp_genes=None, mult=1.0, seed=0, bias=True, trace_cap=0, horizon=0):
+class limits:
+    """Context manager: the episode limits (or_set_limits; TIMEOUT_THRESH and
+    WIN_SCORE of config.py, pg_eval_args.timeout_thresh / win_score) for the
+    calls inside it; 0 = the reference's 2000 / 3."""
+
+    def __init__(self, timeout_thresh=0, win_score=0):
+        self.t, self.w = int(timeout_thresh), int(win_score)
+
+    def __enter__(self):
+        lib().or_set_limits(self.t, self.w)
+        return self
+
+    def __exit__(self, *exc):
+        lib().or_set_limits(0, 0)
+        return False
+
+
+def play_game(genes, nodes, opp_kind, opp_genes=None, mult=1.0, seed=0, bias=True, trace_cap=0, horizon=0,
+              timeout_thresh=0, win_score=0):
     """One game slot (or_play_slot): a perform_episode, or with ``horizon`` > 0
     the fixed-horizon mode (T frames, auto-reset; pong_ga.h pg_eval_args.horizon)."""
+    with limits(timeout_thresh, win_score):
+        return _play_game(genes, nodes, opp_kind, opp_genes, mult, seed, bias, trace_cap, horizon)
+
+
+def _play_game(genes, nodes, opp_kind, opp_genes, mult, seed, bias, trace_cap, horizon):
     net = Net(nodes, bias)
     g = np.ascontiguousarray(genes, dtype=np.float64)
     og = np.ascontiguousarray(opp_genes, dtype=np.float64) if opp_genes is not None else None
@@ -188,9 +213,16 @@ def play_game(genes, nodes, opp_kind, opp_genes=None, mult=1.0, seed=0, bias=Tru
 
 
 def eval_population(genomes, nodes, kind, opp_index, mult, opponents=None, bias=True,
-                    base_seed=0, n_threads=0, horizon=0):
+                    base_seed=0, n_threads=0, horizon=0, timeout_thresh=0, win_score=0):
     """Whole-population evaluate(): returns a dict of numpy arrays (``horizon`` > 0:
-    every game slot in the fixed-horizon mode, or_eval_population_h)."""
+    every game slot in the fixed-horizon mode, or_eval_population_h; ``timeout_thresh``,
+    ``win_score``: config.py's TIMEOUT_THRESH / WIN_SCORE, 0 = the reference's)."""
+    with limits(timeout_thresh, win_score):
+        return _eval_population(genomes, nodes, kind, opp_index, mult, opponents, bias, base_seed, n_threads,
+                                horizon)
+
+
+def _eval_population(genomes, nodes, kind, opp_index, mult, opponents, bias, base_seed, n_threads, horizon):
     net = Net(nodes, bias)
     G = np.ascontiguousarray(genomes, dtype=np.float64)
     n = G.shape[0]

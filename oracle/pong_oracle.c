@@ -26,6 +26,13 @@ uint64_t or_game_seed(uint64_t base_seed, int game_index) {
   return or_splitmix64(base_seed ^ (0xA24BAED4963EE407ull * (uint64_t)(game_index + 1)));
 }
 
+static int or_timeout_thresh = OR_TIMEOUT_THRESH, or_win_score = OR_WIN_SCORE;
+
+void or_set_limits(int timeout_thresh, int win_score) {
+  or_timeout_thresh = timeout_thresh > 0 ? timeout_thresh : OR_TIMEOUT_THRESH;
+  or_win_score = win_score > 0 ? win_score : OR_WIN_SCORE;
+}
+
 static int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 void or_env_reset(or_pong_state *s, uint64_t game_seed, int one_player) {
@@ -357,8 +364,8 @@ void or_play_slot(const double *genes, const or_net *net, int opp_kind, const do
     last1 = s.score1;
     last2 = s.score2;
     /* termination main.py:102-107 */
-    const int ep_end = s.score1 >= OR_WIN_SCORE || s.score2 >= OR_WIN_SCORE || or_env_done(&s) ||
-                       timeout > (double)OR_TIMEOUT_THRESH;
+    const int ep_end = s.score1 >= or_win_score || s.score2 >= or_win_score || or_env_done(&s) ||
+                       timeout > (double)or_timeout_thresh;
     if (horizon <= 0) {
       if (ep_end) break;
       continue;

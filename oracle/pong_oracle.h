@@ -53,6 +53,11 @@ extern "C" {
 /* ---- episode constants (config.py) ---- */
 #define OR_WIN_SCORE 3          /* config.py:53 */
 #define OR_TIMEOUT_THRESH 2000  /* config.py:28 */
+/* The episode limits every later or_play_* call uses (perform_episode's
+ * termination, main.py:102-107; pg_eval_args.timeout_thresh / win_score):
+ * 0 restores the reference's values above.  Not thread-safe: set it before
+ * the calls, not during a parallel evaluation. */
+void or_set_limits(int timeout_thresh, int win_score);
 
 /* opponent kinds for the LEFT paddle (the genome always plays the right paddle) */
 enum {

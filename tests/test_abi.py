@@ -159,7 +159,7 @@ def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
 
 
 def test_struct_size_refuses_other_layouts(lib):
-    """ABI 10: pg_eval_args.struct_size must be this header's sizeof; a short
+    """ABI 10+: pg_eval_args.struct_size must be this header's sizeof; a short
     (or long) struct is refused before any other field is read, and so is the
     ABI-9 layout, whose first word (net.n_nodes) lands in struct_size."""
     from pong_amd import _lib
@@ -174,8 +174,17 @@ def test_struct_size_refuses_other_layouts(lib):
         assert b"struct_size" in lib.pg_last_error()
         assert lib.pg_eval_workspace_bytes(ctypes.byref(a)) == 0
 
+    class Abi10(ctypes.Structure):  # round 5's layout: ends at horizon (no episode limits)
+        _fields_ = [f for f in _lib.PgEvalArgs._fields_ if f[0] not in ("timeout_thresh", "win_score")]
+    a10 = Abi10()
+    a10.struct_size = ctypes.sizeof(Abi10)
+    a10.net = _lib.make_net([6, 2, 2])
+    a10.n_games, a10.n_genomes = 6, 0
+    rc = lib.pg_eval_population(ctypes.cast(ctypes.byref(a10), ctypes.POINTER(_lib.PgEvalArgs)), None)
+    assert rc == _lib.PG_ERR_INVALID and b"struct_size" in lib.pg_last_error()
+
     class Abi9(ctypes.Structure):  # round 4's layout: no struct_size, ends at horizon
-        _fields_ = [f for f in _lib.PgEvalArgs._fields_ if f[0] != "struct_size"]
+        _fields_ = [f for f in Abi10._fields_ if f[0] != "struct_size"]
     old = Abi9()
     old.net = _lib.make_net([6, 64, 3])
     old.n_games, old.n_genomes = 6, 0

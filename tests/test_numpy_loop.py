@@ -89,3 +89,67 @@ def test_timed_rate_solo_leg_same_sample():
     assert len(out) == 5
     rate_s, steps_s, games_s, dt_s, w0 = out[4]
     assert rate_s > 0 and steps_s > 0 and games_s > 0 and w0 > 0
+
+
+def _timeout_points(trace, thresh):
+    """Frames of points whose no-score counter (main.py:128-135) would have
+    passed ``thresh`` on that very frame: the point resets it first
+    (main.py:94-107), so the game goes on unless a score reached WIN_SCORE."""
+    vis = (np.asarray(trace) >> 4) & 1
+    last, out = 1, []
+    for f in range(2, len(vis) + 1):
+        if vis[f - 2] == 1 and vis[f - 1] == 0:  # the ball vanished on frame f: a point
+            if f - last == thresh + 1:
+                out.append(f)
+            last = f
+    return out
+
+
+@pytest.mark.parametrize("thresh,win", [(59, 0), (119, 0), (0, 1), (0, 2), (59, 5)])
+def test_episode_limits_match_oracle(thresh, win):
+    """config.py's TIMEOUT_THRESH / WIN_SCORE (pg_eval_args.timeout_thresh /
+    win_score): the numpy restatement of perform_episode (main.py:69-112) and
+    the C oracle agree at other values than the reference's 2000 / 3 -- in
+    particular on points that land on the frame the no-score counter would
+    pass the threshold (counter reset first, main.py:94-107)."""
+    rng = np.random.default_rng(31 + thresh + win)
+    shape = [6, 8, 3]
+    G = 7 * 8 + 9 * 3
+    genomes = rng.standard_normal((2, G)) * 3
+    opponents = rng.standard_normal((2, G)) * 3
+    kinds = np.tile(np.array([0, 1, 2, 3, 3, 3], np.int32), (2, 1))
+    opp = rng.integers(0, 2, (2, 6)).astype(np.int32)
+    mult = np.where(kinds == 3, 0.7, 1.0)
+    ref = O.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents, timeout_thresh=thresh,
+                            win_score=win)
+    for i in range(2):
+        fit, rew, frames = NL.evaluate(shape, genomes[i], kinds[i], opp[i], mult[i], opponents,
+                                       timeout_thresh=thresh or None, win_score=win or None)
+        np.testing.assert_array_equal(np.array(rew, dtype=np.float64), ref["rewards"][i])
+        assert fit == ref["fitness"][i]
+        assert frames == int(ref["frames"][i].sum())
+    if win:
+        assert ref["scores"].max() <= max(win, 1)
+    # the limits are restored after the call
+    d = O.eval_population(genomes[:1], shape, kinds[:1], opp[:1], mult[:1], opponents=opponents)
+    d0 = O.eval_population(genomes[:1], shape, kinds[:1], opp[:1], mult[:1], opponents=opponents,
+                           timeout_thresh=2000, win_score=3)
+    np.testing.assert_array_equal(d["frames"], d0["frames"])
+
+
+def test_timeout_points_exist_at_thresh_59():
+    """The GPU limit tests (test_gpu_limits.py) run at TIMEOUT_THRESH = 59
+    because N(0, 3) self-play puts points on the 60th frame of a rally often
+    (serve delay 30 + a crossing): the threshold case is exercised, and the
+    oracle plays on past it."""
+    rng = np.random.default_rng(3)
+    G = 7 * 64 + 65 * 3
+    n_ev = 0
+    for i in range(12):
+        r, l_ = rng.standard_normal(G) * 3, rng.standard_normal(G) * 3
+        for g in range(6):
+            res = O.play_game(r, [6, 64, 3], O.OPP_NN, l_, 1.0, O.game_seed(0, g), trace_cap=20000,
+                              timeout_thresh=59)
+            ev = _timeout_points(res["trace"], 59)
+            n_ev += sum(1 for f in ev if f < res["frames"])
+    assert n_ev > 0
