@@ -145,6 +145,9 @@ def main():
     ga.ev.horizon = args.horizon  # pg_eval_args.horizon: 0 = evaluate()'s episodes
     ga.order_by_length = os.environ.get("PG_NO_LENGTH_ORDER") != "1"  # A/B switch for the evaluation order
     ga.early_prep = os.environ.get("PG_NO_EARLY_PREP") != "1"  # A/B switch: schedule + genome records during the HoF scan
+    # config 5 (strong scaling): each rank plays an equal share of long and short
+    # genomes, dealt by predicted game length (DeviceGA.balance_shards; N > 1 only)
+    ga.balance_shards = args.config == "wide" and os.environ.get("PG_NO_BALANCE") != "1"
     G = ga.G
     ga.initialize("normal" if args.dist == "normal" else "uniform", args.sigma)
     # the first games already face a full hall of fame: H independent random

@@ -51,6 +51,32 @@ def gather_fitness(local: torch.Tensor, n_total: int, group=None) -> torch.Tenso
     return torch.cat(parts).to(local.device)
 
 
+def gather_equal(local: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather equal-sized per-rank tables ([n, ...] each) into [world * n, ...],
+    rank-major: the length-balanced shards' (row, fitness, longest game) entries
+    (evolve.DeviceGA.balance_shards), whose rows are dealt, not contiguous."""
+    world = dist.get_world_size(group)
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if stage else local.device
+    buf = local.to(dev).contiguous()
+    out = torch.empty((local.shape[0] * world,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    if stage:
+        dist.all_gather(list(out.split(local.shape[0])), buf, group=group)
+    else:
+        dist.all_gather_into_tensor(out, buf, group=group)
+    return out.to(local.device)
+
+
+def deal_positions(n_buf: int, rank: int, world: int, device=None) -> torch.Tensor:
+    """Positions of rank ``rank`` in a snake deal of a length-ordered list over
+    ``world`` ranks: round k gives position k * world + (rank if k is even else
+    world - 1 - rank), so each rank's k-th game is as long as the others' (the
+    longest first) and the per-rank totals stay within one game's length."""
+    k = torch.arange(n_buf, device=device, dtype=torch.int64)
+    off = torch.where(k % 2 == 0, torch.full_like(k, rank), torch.full_like(k, world - 1 - rank))
+    return k * world + off
+
+
 def gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     """All-gather each rank's shard rows ([rows, ...]) into the full table in
     row order (gather_fitness for any row width: genomes, hashes)."""

@@ -141,6 +141,16 @@ class DeviceGA:
         # sharded variation (module docstring; fused path): at N = 1 the shard is
         # the whole population and there is nothing to leave out
         self.shard_vary = self.world > 1
+        # Length-balanced shards (fused path, N > 1; BASELINE config 5's strong
+        # scaling): a generation's invalid rows, ordered longest predicted game
+        # first over the whole population (the lineage is replicated: the
+        # all-gather carries it), are dealt to the ranks in snake order, so every
+        # rank plays an equal share of long and short genomes and the slowest
+        # rank -- the generation's pace -- waits for no unlucky contiguous shard.
+        # A rank still varies its contiguous shard (shard_rows() and
+        # population_full() stay as they are) and also the rows dealt to it.
+        self.balance_shards = False
+        self._dealt = {}  # generation parity -> pair mask of the rows dealt to this rank
         self._n_pairs = (self.P + 1) // 2
         self._skip = (self.lo >> 1, (self.hi + 1) >> 1) if self.hi > self.lo else (0, 0)
         self._shard_pairs = None
@@ -171,8 +181,19 @@ class DeviceGA:
         kw = {}
         if self.hof_slices > 1:
             kw = dict(hof_slices=self.hof_slices, block_rows=self.hof_block_rows, slice_local=self._sliced(n_hof))
-        return D.schedule(self.schedule, self.hi - self.lo, self.n_games, self.lo, self.hof_fitness, n_hof, self.seed,
+        n = rows.shape[0] if rows is not None else self.hi - self.lo
+        return D.schedule(self.schedule, n, self.n_games, self.lo, self.hof_fitness, n_hof, self.seed,
                           g, self.device, rows=rows, **kw)
+
+    def _balanced(self) -> bool:
+        # (not with a sliced hall: there a rank's opponents are its row block's slice)
+        return bool(self.balance_shards and self.fused and self.world > 1 and dist.is_initialized()
+                    and self.hof_slices == 1)
+
+    @property
+    def _n_eval(self) -> int:
+        """Entries of this rank's evaluation: its shard, or (balanced) ceil(P / N) dealt rows."""
+        return -(-self.P // self.world) if self._balanced() else self.hi - self.lo
 
     # ------------------------------------------------------------ views
     @property
@@ -539,6 +560,40 @@ class DeviceGA:
                invalid=self._buf("complete_inv_" + name, self.P, torch.uint8))
         return mask
 
+    def _deal(self, inv_u8: torch.Tensor, g: int):
+        """Length-balanced shards: this rank's evaluation order (rows, count) --
+        the invalid rows of the whole population longest lineage first (ties by
+        row, pg_ga_order), dealt in snake order over the ranks (dist.deal_positions)."""
+        P = self.P
+        grows = self._buf("deal_rows", P, torch.int32)
+        gcount = self._buf("deal_count", 1, torch.int32)
+        D.order(P, 0, inv_u8, self.lineage_frames, True, grows, gcount, self.ws)
+        n = self._n_eval
+        pos = PD.deal_positions(n, self.rank, self.world, self.device)
+        local = self._buf("local_rows%d" % (g & 1), n, torch.int32)
+        local.copy_(grows[pos.clamp(max=P - 1)])
+        count = self._buf("local_count%d" % (g & 1), 1, torch.int32)
+        count.copy_((pos < gcount.long()).sum().to(torch.int32).reshape(1))  # a prefix: pos grows with k
+        return local, count
+
+    def _gather_dealt(self, res, local: torch.Tensor, count: torch.Tensor) -> torch.Tensor:
+        """The balanced evaluation's all-gather: every rank's (row, fitness,
+        longest game) entries, scattered into the population's fitness (rows
+        nobody played read 0) and lineage (played rows' longest games)."""
+        P, n = self.P, local.shape[0]
+        played = torch.arange(n, device=self.device) < count
+        rid = torch.where(played, local.long(), torch.full_like(local, P, dtype=torch.int64))
+        longest = res.frames.max(dim=1).values.double()
+        pack = torch.stack([rid.double(), res.fitness, longest], dim=1)
+        allp = PD.gather_equal(pack, self.group)
+        at = allp[:, 0].long()  # (unplayed entries land in the dropped slot P)
+        fit = torch.zeros(P + 1, dtype=torch.float64, device=self.device)
+        fit.index_copy_(0, at, allp[:, 1])
+        lin = torch.cat([self.lineage_frames, self.lineage_frames.new_zeros(1)])
+        lin.index_copy_(0, at, allp[:, 2].float())
+        self.lineage_frames.copy_(lin[:P])
+        return fit[:P]
+
     def _next_gen_prep(self, g: int, parents: torch.Tensor, fitness: torch.Tensor, store: torch.Tensor,
                        cand_pairs: Optional[torch.Tensor] = None):
         """Generation g's selTournament + varAnd into store[H:] (sharded: this
@@ -549,14 +604,23 @@ class DeviceGA:
         parents, from store[H:] (generation g - 2) before it is overwritten."""
         chosen = self._select(g, fitness)
         if cand_pairs is not None:
-            self._complete(g - 1, parents, store[self.H:], chosen, "parents", exclude=cand_pairs)
+            # generation g - 1's pairs already current here: the shard's (skip), the
+            # candidates' and (balanced) the rows dealt to this rank
+            prev = self._dealt.get((g - 1) & 1)
+            self._complete(g - 1, parents, store[self.H:], chosen, "parents",
+                           exclude=cand_pairs if prev is None else (cand_pairs | prev))
         _, inv = D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu, self.sigma, self.indpb,
                         seed=self.seed, generation=g, out=store[self.H:],
                         pair_mask=self._shard_mask() if self._sharded() else None)
         inherited = self._buf("inherited", self.P, torch.float64)
         D.inherit(chosen, fitness, inherited, self.lineage_frames, self._lineage_alt)
         self.lineage_frames, self._lineage_alt = self._lineage_alt, self.lineage_frames
-        order = self._order(inv, g)
+        if self._balanced():
+            order = self._deal(inv, g)
+            if self._sharded():  # the dealt rows beyond the shard, varied like a completion
+                self._dealt[g & 1] = self._complete(g, store[self.H:], parents, order[0], "dealt%d" % (g & 1))
+        else:
+            order = self._order(inv, g)
         self._next = (g, inv, inherited, order, self._early_prep(g, store[self.H:], order))
 
     def _early_prep(self, g: int, off: torch.Tensor, order):
@@ -565,7 +629,7 @@ class DeviceGA:
         updated hall of fame: a self-play schedule against a full hall of fame
         (its size stays H, and self-play opponents are picked by index only).
         Returns the schedule for _evaluate_fused, or None."""
-        n = self.hi - self.lo
+        n = self._n_eval
         if (not self.early_prep or self.schedule != "selfplay" or self.H == 0 or self.hof_n != self.H or self.last is None
                 or self.last.fitness.shape[0] != n):
             return None
@@ -588,7 +652,7 @@ class DeviceGA:
 
     def _evaluate_fused(self, g: int, rows: torch.Tensor, order, sched=None) -> torch.Tensor:
         lo, hi = self.lo, self.hi
-        n = hi - lo
+        n = self._n_eval
         local, count = order
         if sched is None:
             kind, opp, mult = self.eval_schedule(g, rows=local)
@@ -606,6 +670,8 @@ class DeviceGA:
         self.last, self.last_rows, self.last_count = res, local, count
         if self.on_evaluate is not None:
             self.on_evaluate(g, rows, opponents, res)
+        if self._balanced():
+            return self._gather_dealt(res, local, count)
         shard = self._buf("shard_fit", n, torch.float64)
         D.scatter_fitness(res, n, lo, local, count, shard, self.lineage_frames)
         if not dist.is_initialized():
@@ -720,7 +786,7 @@ class DeviceGA:
         worst = float(self._hof_fit_host[-1]) if (self.H and self.hof_n >= self.H) else None
         if self.generation < 0:
             inv = (~self.valid).to(torch.uint8)
-            fit = self._evaluate_fused(0, self._rows, self._order(inv))
+            fit = self._evaluate_fused(0, self._rows, self._deal(inv, 0) if self._balanced() else self._order(inv))
             new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, self.fitness, worst)
             self.fitness, self.valid = new_fit, torch.ones_like(self.valid)
             # generation 1's offspring go to spare[H:] (no swap after the initial
@@ -748,7 +814,8 @@ class DeviceGA:
             # the side stream (_next_gen_prep), both before generation g + 1's
             # variation overwrites store[H:]
             # (no hall of fame: the candidates are never read)
-            cand_pairs = self._complete(g, off, self._rows, cand[:k] if self.H else cand[:0], "cand")
+            cand_pairs = self._complete(g, off, self._rows, cand[:k] if self.H else cand[:0], "cand",
+                                        exclude=self._dealt.get(g & 1) if self._balanced() else None)
             self._mark("complete", sub=True)
         # generation g + 1's parents are this offspring; its offspring go to
         # store[H:] (this generation's parents, free now), the buffer the swap

@@ -30,7 +30,10 @@ def find_stuff(observation):
     dev = torch.device(DEVICE)  # noqa: F405
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
-    frame = torch.as_tensor(np.ascontiguousarray(observation, dtype=np.uint8), device=dev)
+    if isinstance(observation, torch.Tensor):  # a DeviceEnv frame: already on the device
+        frame = observation.to(device=dev, dtype=torch.uint8).contiguous()
+    else:
+        frame = torch.as_tensor(np.ascontiguousarray(observation, dtype=np.uint8), device=dev)
     got = _device.find_stuff(frame)[0].cpu().numpy()
     if not np.isnan(got).any():
         return got

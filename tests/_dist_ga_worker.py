@@ -5,6 +5,10 @@ saves the final state.
 usage: python _dist_ga_worker.py OUT_DIR            (small: [6,8,3], P 101, 3 generations)
        python _dist_ga_worker.py OUT_DIR config4    (BASELINE config 4: [6,64,3], P 524 288,
                                                      self-play vs P/4 hall of fame, 2 generations)
+       python _dist_ga_worker.py OUT_DIR wide       (BASELINE config 5's [6,512,512,3], f32, P 256,
+                                                     self-play vs a 64-row hall, 2 generations;
+                                                     wide_balanced: the length-balanced shards)
+       python _dist_ga_worker.py OUT_DIR slices     ([6,8,3], P 96, hall of 3 < 4 row blocks)
 At world > 1 DeviceGA varies only each rank's shard (shard_vary).
 """
 import json
@@ -72,6 +76,60 @@ def main(out_dir, mode="small"):
             with open(os.path.join(out_dir, "profile.json"), "w") as fh:
                 json.dump({"world": world, "rank_rows": ga.hi - ga.lo, "generation1_ms": step_ms,
                            "generation1_phases_ms": phases, "logbook": ga.logbook}, fh)
+    elif mode in ("wide", "wide_balanced"):
+        # BASELINE config 5's network [6,512,512,3] (f32 genomes, k_wide) at a small
+        # population, self-play vs the hall of fame: the 1 -> N strong-scaling split
+        P = 256
+        ga = DeviceGA([6, 512, 512, 3], P, hof_size=64, tournsize=64, dtype=torch.float32, device=dev,
+                      schedule="selfplay", seed=9)
+        ga.balance_shards = mode == "wide_balanced"
+        ga.initialize("normal", 3.0)
+        sample = {}
+
+        def keep(g, rows, opponents, res):  # 4 of this rank's evaluated genomes, for an oracle replay
+            n = res.fitness.shape[0]
+            played = int(ga.last_count[0]) if ga.last_count is not None else n
+            pick = np.arange(min(4, played))
+            pt = torch.as_tensor(pick, device=dev)
+            r = ga.last_rows[pt].long() if ga.last_rows is not None else pt
+            kind, opp, mult = ga.eval_schedule(g)
+            o = opp[pt].cpu().numpy()
+            used = np.unique(o)
+            sample.update(genomes=rows[r].double().cpu().numpy(), kind=kind[pt].cpu().numpy(),
+                          opp=np.searchsorted(used, o).astype(np.int32), mult=mult[pt].cpu().numpy(),
+                          opponents=(opponents[torch.as_tensor(used, device=dev)].double().cpu().numpy()
+                                     if opponents is not None else np.zeros((1, ga.G))),  # (generation 0: no hall yet)
+                          fitness=res.fitness[pt].cpu().numpy(), frames=res.frames[pt].cpu().numpy())
+        ga.on_evaluate = keep
+        ga.run(2)
+        h = ga.population_hash().cpu().numpy()
+        if not dist.is_initialized() or dist.get_rank() == 0:
+            os.makedirs(out_dir, exist_ok=True)
+            np.save(os.path.join(out_dir, "pop_hash.npy"), h)
+            np.save(os.path.join(out_dir, "fitness.npy"), ga.fitness.cpu().numpy())
+            np.save(os.path.join(out_dir, "hof_hash.npy"), D.row_hash(ga.hall_of_fame, ga.G).cpu().numpy())
+            np.save(os.path.join(out_dir, "hof_fitness.npy"), ga.hof_member_fitness)
+            np.savez(os.path.join(out_dir, "sample.npz"), **sample)
+            with open(os.path.join(out_dir, "profile.json"), "w") as fh:
+                json.dump({"world": world, "logbook": ga.logbook}, fh)
+    elif mode == "slices":
+        # a sliced hall (pg_schedule_args.hof_slices) with fewer members than row
+        # blocks: P = 96 in 4 blocks of 24, a 3-member hall -> K = 3 slices, and
+        # block 3 plays slice 3 mod 3 = 0 (round-5 review: rank 3 had passed an
+        # empty slice); each of 4 ranks holds one block
+        ga = DeviceGA([6, 8, 3], 96, hof_size=3, tournsize=9, device=dev, schedule="selfplay", seed=21,
+                      hof_block_rows=24)
+        ga.initialize("normal", 2.0)
+        ga.run(3)
+        pop = ga.population_full().cpu().numpy()
+        if not dist.is_initialized() or dist.get_rank() == 0:
+            os.makedirs(out_dir, exist_ok=True)
+            np.save(os.path.join(out_dir, "population.npy"), pop)
+            np.save(os.path.join(out_dir, "fitness.npy"), ga.fitness.cpu().numpy())
+            np.save(os.path.join(out_dir, "hof.npy"), ga.hall_of_fame.cpu().numpy())
+            np.save(os.path.join(out_dir, "hof_fitness.npy"), ga.hof_member_fitness)
+            np.save(os.path.join(out_dir, "rows.npy"), np.array([ga.lo, ga.hi, ga.hof_slices,
+                                                                 -1 if ga._slice is None else ga._slice]))
     else:
         ga = DeviceGA([6, 8, 3], 101, hof_size=20, tournsize=9, device=dev, schedule="reference", seed=77)
         ga.initialize("normal", 2.0)

@@ -68,3 +68,45 @@ def test_two_rank_sharded_evaluation(oracle, tmp_path, n):
              nprocs=2, join=True)
     single = oracle.eval_population(genomes, shape, kinds, opp, mult, opponents=opponents)["fitness"]
     np.testing.assert_array_equal(np.load(out), single)
+
+
+def test_deal_positions_snake_partition():
+    """The length-balanced shards' deal (DeviceGA.balance_shards): the ranks'
+    positions partition [0, N * n), each rank's k-th position lies in round k,
+    and a descending list dealt this way leaves the ranks' sums within one
+    element of each other."""
+    from pong_amd.dist import deal_positions
+    rng = np.random.default_rng(0)
+    for world in (1, 2, 3, 8):
+        n = 13
+        pos = [deal_positions(n, r, world).numpy() for r in range(world)]
+        allp = np.sort(np.concatenate(pos))
+        np.testing.assert_array_equal(allp, np.arange(world * n))
+        for p in pos:
+            np.testing.assert_array_equal(p // world, np.arange(n))
+        lengths = np.sort(rng.integers(1, 2000, size=world * n))[::-1]
+        sums = [lengths[p].sum() for p in pos]
+        assert max(sums) - min(sums) <= lengths[0]
+
+
+def _gather_equal_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path.insert(0, os.path.join(os.path.dirname(here), "neuro-genetic-pong-self-play_amd"))
+        from pong_amd.dist import gather_equal
+        local = torch.tensor([[rank, 10.0 * rank + k] for k in range(3)], dtype=torch.float64)
+        out = gather_equal(local)
+        if rank == 0:
+            np.save(out_path, out.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_equal_two_ranks(tmp_path):
+    out = str(tmp_path / "g.npy")
+    mp.spawn(_gather_equal_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    np.testing.assert_array_equal(got, np.array([[0, 0], [0, 1], [0, 2], [1, 10], [1, 11], [1, 12]], np.float64))

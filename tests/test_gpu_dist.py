@@ -80,3 +80,47 @@ def test_config4_sharded_524k_equals_single_process(gpu, oracle, tmp_path):
     if os.path.isdir(os.path.join(repo, "gpurun_out")):
         with open(os.path.join(repo, "gpurun_out", "config4_profile.json"), "w") as fh:
             json.dump(rec, fh, indent=1)
+
+
+def test_wide_config5_split_equals_single_process(gpu, oracle, tmp_path):
+    """BASELINE config 5's 1 -> N split: the [6,512,512,3] network (f32 genomes,
+    k_wide), P = 256 self-play vs a 64-row hall, two generations, at 1 rank, 2
+    ranks (contiguous shards) and 2 and 8 ranks with length-balanced shards
+    (the rows dealt by predicted game length, DeviceGA.balance_shards) -- every
+    run ends in the same population, fitness and hall of fame, and 4 of rank
+    0's last evaluated genomes are re-played by the oracle."""
+    import json
+    outs = {}
+    for world, mode in ((1, "wide"), (2, "wide"), (2, "wide_balanced"), (8, "wide_balanced")):
+        out = str(tmp_path / f"{mode}{world}")
+        _run(world, out, mode, timeout=600)
+        outs[(world, mode)] = {k: np.load(os.path.join(out, f"{k}.npy"))
+                               for k in ("pop_hash", "fitness", "hof_hash", "hof_fitness")}
+        with open(os.path.join(out, "profile.json")) as fh:
+            outs[(world, mode)]["logbook"] = json.load(fh)["logbook"]
+        smp = dict(np.load(os.path.join(out, "sample.npz")))
+        ref = oracle.eval_population(smp["genomes"], [6, 512, 512, 3], smp["kind"], smp["opp"], smp["mult"],
+                                     opponents=smp["opponents"], n_threads=8)
+        np.testing.assert_array_equal(smp["fitness"], ref["fitness"], err_msg=f"{mode} {world}")
+        np.testing.assert_array_equal(smp["frames"], ref["frames"], err_msg=f"{mode} {world}")
+    base = outs[(1, "wide")]
+    for key, o in outs.items():
+        for k in ("pop_hash", "fitness", "hof_hash", "hof_fitness"):
+            np.testing.assert_array_equal(o[k], base[k], err_msg=f"{k} at {key}")
+        assert o["logbook"] == base["logbook"], key
+
+
+def test_sliced_hall_smaller_than_blocks(gpu, tmp_path):
+    """A sliced hall with fewer members than row blocks (P = 96 in four
+    24-row blocks, a 3-member hall: K = 3, block 3 plays slice 0): four ranks,
+    one block each, each passing only its slice, end three generations equal to
+    the single process that passes the whole hall (round-5 review)."""
+    outs = {}
+    for world in (1, 4):
+        out = str(tmp_path / f"s{world}")
+        _run(world, out, "slices")
+        outs[world] = {k: np.load(os.path.join(out, f"{k}.npy"))
+                       for k in ("population", "fitness", "hof", "hof_fitness", "rows")}
+    assert tuple(outs[4]["rows"][2:]) == (3, 0)  # rank 0: 3 slices, its block 0 plays slice 0
+    for k in ("population", "fitness", "hof", "hof_fitness"):
+        np.testing.assert_array_equal(outs[4][k], outs[1][k], err_msg=k)

@@ -167,3 +167,20 @@ def test_replay_game_seed_matches_oracle(oracle):
     for base in (0, 1, 12345, 2**63 + 7, 2**64 - 1):
         for g in range(8):
             assert game_seed(base, g) == oracle.lib().or_game_seed(base, g)
+
+
+def test_human_input_key_sources():
+    """human_control.HumanInput (human_control.py:26-36): run() returns the held
+    [w, s] keys as [up, down]; headless, the keys come from a callable of
+    (call index, input vector) or an iterable (exhausted = nothing held);
+    without a key source it needs pynput's keyboard, which is absent here."""
+    import human_control
+    h = human_control.HumanInput(keys=lambda f, x: (f % 2, x[1] > 0.5))
+    assert h.run([0, 0.9, 0, 0, 0, 0]) == [0, 1] and h.run([0, 0.1, 0, 0, 0, 0]) == [1, 0] and h.frame == 2
+    h = human_control.HumanInput(keys=[(1, 0), (1, 1)])
+    assert h.run() == [1, 0] and h.run() == [1, 1] and h.run() == [0, 0]
+    try:
+        import pynput  # noqa: F401
+    except ImportError:
+        with pytest.raises(RuntimeError):
+            human_control.HumanInput()
