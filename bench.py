@@ -180,6 +180,7 @@ def main():
     hidden_local = 0        # serve-delay frames advanced at once (counters[12])
     counters = []
     events = []
+    probe_local = [0, 0, 0]  # diagnostic builds (PG_DECIDE_PROBE, PG_START_PROBE): counters[13..15]
     for s in range(args.steps):
         # a fresh pair per step, read after the timed region: no per-step sync
         ga.eval_events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -203,6 +204,7 @@ def main():
         passes_local += int(c[7])
         skip_local += int(c[8])
         hidden_local += int(c[12])
+        probe_local = [a + int(v) for a, v in zip(probe_local, c[13:16])]
 
     t = torch.tensor([elapsed, float(steps_local), float(fwd_local), float(slow_local), sum(kernel_ms)]
                      + [float(v) for v in cert_local] + [float(passes_local), float(skip_local),
@@ -290,7 +292,8 @@ def main():
                        "certificate_failures_per_forward": cert_all[0] / max(fwd_all, 1.0),
                        "failures_decided_in_wave": cert_all[2] / max(cert_all[0], 1.0),
                        "failures_decided_by_f64_certificate": cert_all[1] / max(cert_all[0], 1.0),
-                       "numpy_order_f64_forwards_per_forward": slow_all / max(fwd_all, 1.0)},
+                       "numpy_order_f64_forwards_per_forward": slow_all / max(fwd_all, 1.0),
+                       **({"probe_counters_13_15": probe_local} if probe_local[2] else {})},
             "roofline": _selfplay_roofline(args, G, dtype, achieved_tflops, kernel_ms_mean, flops_per_forward,
                                            fwd_per_launch, steps_per_launch, streaming_bytes, n_local, H),
         }

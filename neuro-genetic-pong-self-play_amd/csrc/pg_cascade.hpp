@@ -529,7 +529,7 @@ __device__ __forceinline__ int certify_c8(const float z[O], const Cert &c) {
     return ok ? wc : -1;
 #else
     const bool m0 = z[0] >= c.tlo, m1 = z[1] >= c.tlo;  // (with top1 >= tlo one of the three is)
-    const int fc = m0 ? 8 : (m1 ? 16 : 0);
+    const int fc = m0 ? -6 : (m1 ? 6 : 0);  // index_to_move of the first maybe-saturated output
     const float zf = m0 ? z[0] : (m1 ? z[1] : z[2]);
     const int sat_res = zf > c.thi ? fc : -1;
     const int uns_res = (top1 - top2 > c.e2 + tw && top1 > c.lowz) ? wc : -1;
@@ -539,6 +539,45 @@ __device__ __forceinline__ int certify_c8(const float z[O], const Cert &c) {
     const int idx = certify_c<O>(z, c);
     return idx < 0 ? -1 : index_to_move(idx);
   }
+}
+
+// The gap rule of certify_c with the plateau width at its true size, for the
+// frames certify_c8 leaves undecided in the plateau regime (k_service's rare
+// block, before plateau_f32).  When both of the two largest outputs are in the
+// regime (top2 - e >= 22.2: S = 1 - m 2^-52, m = rint(2^52 pow(e, -z)), pow
+// within 1 ulp), the winner's m is strictly the smaller -- its S strictly the
+// larger -- once 2^52 (e^-(top2 + e) (1 - 2^-52) - e^-(top1 - e) (1 + 2^-52)) > 1,
+// which holds when top1 - top2 > 2e + 2^-52 e^top1 + 2^-51 (ln(1 + x) <= x).
+// certify_c prices the width at 4 2^-52 (e^(top1 + e) + 1), valid at every z;
+// here it is 2^-52 e^top1 x 1.01 (the f32 exponent's and v_exp_f32's error,
+// ~2e-6 relative) -- about 4x fewer undecided frames in populations evolved
+// from U[0,1) genes (ga.py:85), no transcendental beyond the one exp2.
+// Returns the paddle move (index_to_move) or -1.
+template <int O>
+__device__ __forceinline__ int tight_gap_move(const float z[O], float e, const Cert &c) {
+  float top1, top2;
+  int w;
+  if constexpr (O == 3) {
+    top1 = fmaxf(fmaxf(z[0], z[1]), z[2]);
+    top2 = __builtin_amdgcn_fmed3f(z[0], z[1], z[2]);
+    w = z[0] == top1 ? 0 : (z[1] == top1 ? 1 : 2);
+  } else {
+    top1 = z[0];
+    top2 = -3.0e38f;
+    w = 0;
+#pragma unroll
+    for (int o = 1; o < O; ++o) {
+      const bool gt = z[o] > top1;
+      top2 = gt ? top1 : fmaxf(top2, z[o]);
+      w = gt ? o : w;
+      top1 = gt ? z[o] : top1;
+    }
+  }
+  // 2^(top1 log2 e - 52 + log2 1.01) + 2^-51; the sum's f32 roundings inside the (1 + 2^-20)
+  const float tw = __builtin_amdgcn_exp2f(__builtin_fmaf(top1, 1.4426950408889634f, -51.985645f)) +
+                   4.4408921e-16f;
+  const bool ok = (top2 - e >= 22.2f) & (top1 < c.tlo) & (top1 - top2 > (2.f * e + tw) * 1.000001f);
+  return ok ? index_to_move(w) : -1;
 }
 
 template <int O>
@@ -807,12 +846,12 @@ __device__ int plateau_decide(const float *z, float e, int lane) {
     const double zz = (double)zo + ((lane & 1) ? (double)e : -(double)e);
     if (zz != zz) {
       amb = true;  // NaN: numpy's NaN rule, in the f64 path
-    } else if (zz >= 22.2) {
+    } else if (zz >= PG_K(22.2)) {
       double t = pg_exp_f64(-zz);
-      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
+      t = fma(t, zz * PG_K(5.318237706605891e-17), t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
       const double v = t * 4503599627370496.0;    // 2^52 p
       const double fr = v - floor(v);
-      amb = fabs(fr - 0.5) < 1e-6;  // too close to a rounding boundary to call
+      amb = fabs(fr - 0.5) < PG_K(1e-6);  // too close to a rounding boundary to call
       m = (int)rint(v);
     }
   }
@@ -893,7 +932,7 @@ __device__ __forceinline__ void f64_unit(const double *x, const double *w1, int 
   // the compact sigmoid (pow(e_d, -a) as exp(-a)(1 + a delta), ~1-2 ulp; the
   // bound above allows 6): no table load on the service's critical path
   double tq = pg_exp_f64(-a);
-  if (tq < INFINITY) tq = fma(tq, a * 5.318237706605891e-17, tq);
+  if (tq < INFINITY) tq = fma(tq, a * PG_K(5.318237706605891e-17), tq);
   sj = 1.0 / (1.0 + tq);
   aj = 4.0 * A + 84.0;
 }
@@ -914,7 +953,7 @@ __device__ int f64_decide_sums(const double *zp, const double *ep, const double 
     const double t = wave_sum_f64(zp[o]);
     const double u = wave_sum_f64(ep[o]);
     z[o] = t + c[o];
-    e[o] = 2.0 * kEps * (u + 2.0 * fabs(c[o])) * 1.001 + 1e-300;
+    e[o] = 2.0 * kEps * (u + 2.0 * fabs(c[o])) * PG_K(1.001) + PG_K(1e-300);
   }
   // m-intervals: lanes 0..2O-1 each evaluate one endpoint (z -/+ e)
   constexpr int kBig = 0x7fffffff;  // below the plateau regime
@@ -928,11 +967,11 @@ __device__ int f64_decide_sums(const double *zp, const double *ep, const double 
     const double zz = (lane & 1) ? zo + eo : zo - eo;
     if (zz != zz) {
       amb = true;  // NaN: numpy's NaN rule, in the full path
-    } else if (zz >= 22.2) {
+    } else if (zz >= PG_K(22.2)) {
       double t = pg_exp_f64(-zz);
-      t = fma(t, zz * 5.318237706605891e-17, t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
+      t = fma(t, zz * PG_K(5.318237706605891e-17), t);  // pow(e_d, -z) to ~1 ulp (the 1e-6 margin covers it)
       const double vv = t * 4503599627370496.0;   // 2^52 p
-      amb = fabs(vv - floor(vv) - 0.5) < 1e-6;
+      amb = fabs(vv - floor(vv) - 0.5) < PG_K(1e-6);
       m = (int)rint(vv);
     } else if (zz >= 22.0) {
       amb = true;  // too close to the regime edge to compare across it
@@ -954,7 +993,7 @@ __device__ int f64_decide_sums(const double *zp, const double *ep, const double 
 #pragma unroll
     for (int o = 1; o < O; ++o)
       if (lane == o) top = z[o] + e[o];
-    const double twl = 8.881784197001252e-16 * (pg_exp_f64(fmin(top, 40.0)) + 1.0);
+    const double twl = 8.881784197001252e-16 * (pg_exp_f64(fmin(top, 40.0)) + 1.0);  // (2^-50: a literal)
     const uint64_t tb = (uint64_t)__double_as_longlong(twl);
 #pragma unroll
     for (int o = 0; o < O; ++o)

@@ -130,6 +130,21 @@ __device__ inline void log_hard(const EvalParams &p, int row, int is_opp, int id
   log_hard_raw(p.hard_log, p.counters, p.hard_cap, row, is_opp, idx, source, k);
 }
 
+// pg_decide's parameters (k_decide, pg_decide.hip: k_service's cascade on given inputs)
+struct DecideParams {
+  const void *genomes;
+  const int32_t *gidx;
+  const int32_t *k;
+  int32_t *index;
+  int32_t *stage;
+  int64_t gstride;
+  int n, H, b;
+};
+// k_decide for the split layout of L lanes per game (pg_decide.hip; its own
+// translation unit, on the default machine scheduler: the iterative-ILP one
+// pong_ga.hip uses for k_service crashes the register allocator on k_decide)
+int32_t launch_decide(const DecideParams &p, int L, int O, bool f64, size_t lds, hipStream_t s);
+
 // [6, H1, H2, O] networks (two hidden layers, H1, H2 <= 512, O in 2..4,
 // n_games <= 8) on the weight-streaming kernel k_wide (pg_wide.hip).
 bool wide_shape_ok(const pg_net &n, int n_games);

@@ -27,6 +27,24 @@
 
 #include <math.h>
 
+/* PG_K(c): an f64 constant of the f64 decision code.  On the device it is
+ * materialized where it is used (its bits plus an opaque zero that a volatile
+ * asm makes there, which no pass hoists): k_service's game loop runs this code in its rare decision
+ * path, and plain constants were hoisted out of the loop into registers that
+ * the allocator then spilled to scratch -- each use a dependent scratch load
+ * inside the decision (tools/isa_frame.py).  Elsewhere (host) the constant. */
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PG_NO_K)  /* PG_NO_K: plain constants (A/B) */
+template <unsigned long long B>
+__device__ __forceinline__ double pg_k64() {
+  unsigned long long zero;  // an opaque 0 made here: B + 0 is not loop-invariant
+  asm volatile("s_mov_b64 %0, 0" : "=s"(zero));
+  return __builtin_bit_cast(double, B + zero);
+}
+#define PG_K(c) (pg_k64<__builtin_bit_cast(unsigned long long, (double)(c))>())
+#else
+#define PG_K(c) (c)
+#endif
+
 /* 2^(j/64), j = 0..63, as hi + lo (hi the nearest double, |lo| < ulp(hi)/2) */
 PG_TABLE double kPgExp2Tbl[128] = {
     1.0, 0.0,
@@ -98,12 +116,12 @@ PG_TABLE double kPgExp2Tbl[128] = {
 /* pow(e_d, -z), e_d = np.e */
 PG_HD double pg_pow_e_neg(double z) {
   if (z != z) return z;
-  if (-z > 709.782712893384) return INFINITY;
-  if (-z < -745.1332191019412) return 0.0;
-  const double kInvL = 92.33248261689366;            /* 64 / ln 2 */
-  const double kLhi = 0.010830424696223417;          /* ln2/64, 36 significant bits: n * kLhi exact */
-  const double kLlo = 2.572804622327669e-14;         /* ln2/64 - kLhi */
-  const double kDelta = 5.318237706605891e-17;       /* 1 - ln(e_d) */
+  if (-z > PG_K(709.782712893384)) return INFINITY;
+  if (-z < PG_K(-745.1332191019412)) return 0.0;
+  const double kInvL = PG_K(92.33248261689366);            /* 64 / ln 2 */
+  const double kLhi = PG_K(0.010830424696223417);          /* ln2/64, 36 significant bits: n * kLhi exact */
+  const double kLlo = PG_K(2.572804622327669e-14);         /* ln2/64 - kLhi */
+  const double kDelta = PG_K(5.318237706605891e-17);       /* 1 - ln(e_d) */
   const double n = rint(-z * kInvL);
   const double r_hi = fma(-n, kLhi, -z);             /* exact: -z - n kLhi */
   const double r_lo = fma(-n, kLlo, z * kDelta);
@@ -112,11 +130,11 @@ PG_HD double pg_pow_e_neg(double z) {
   const double bb = r - r_hi;
   const double re = (r_hi - (r - bb)) + (r_lo - bb);
   /* exp(r + re) = 1 + r + q_lo, q_lo = r^2 P(r) + re (1 + r) */
-  double pp = 1.984126984126984e-04;                 /* 1/5040 */
-  pp = fma(pp, r, 1.388888888888889e-03);            /* 1/720 */
-  pp = fma(pp, r, 8.333333333333333e-03);            /* 1/120 */
-  pp = fma(pp, r, 4.1666666666666664e-02);           /* 1/24 */
-  pp = fma(pp, r, 1.6666666666666666e-01);           /* 1/6 */
+  double pp = PG_K(1.984126984126984e-04);                 /* 1/5040 */
+  pp = fma(pp, r, PG_K(1.388888888888889e-03));            /* 1/720 */
+  pp = fma(pp, r, PG_K(8.333333333333333e-03));            /* 1/120 */
+  pp = fma(pp, r, PG_K(4.1666666666666664e-02));           /* 1/24 */
+  pp = fma(pp, r, PG_K(1.6666666666666666e-01));           /* 1/6 */
   pp = fma(pp, r, 0.5);
   const double q_lo = fma(r * r, pp, re * (1.0 + r));
   const int ni = (int)n;
@@ -140,21 +158,21 @@ PG_HD double pg_sigmoid_f64(double z) {
 
 /* exp(x) to about 1 ulp, small register footprint (error bounds, plateau tests) */
 PG_HD double pg_exp_f64(double x) {
-  if (x > 709.782712893384) return INFINITY;
-  if (x < -745.1332191019412) return 0.0;
-  const double n = rint(x * 1.4426950408889634);
-  const double r = fma(-n, 1.9082149292705877e-10, fma(-n, 6.93147180369123816490e-01, x));
-  double p = 1.6059043836821613e-10;   /* 1/13! */
-  p = fma(p, r, 2.08767569878681e-09);  /* 1/12! */
-  p = fma(p, r, 2.505210838544172e-08); /* 1/11! */
-  p = fma(p, r, 2.755731922398589e-07); /* 1/10! */
-  p = fma(p, r, 2.7557319223985893e-06);
-  p = fma(p, r, 2.48015873015873e-05);
-  p = fma(p, r, 1.984126984126984e-04);
-  p = fma(p, r, 1.388888888888889e-03);
-  p = fma(p, r, 8.333333333333333e-03);
-  p = fma(p, r, 4.1666666666666664e-02);
-  p = fma(p, r, 1.6666666666666666e-01);
+  if (x > PG_K(709.782712893384)) return INFINITY;
+  if (x < PG_K(-745.1332191019412)) return 0.0;
+  const double n = rint(x * PG_K(1.4426950408889634));
+  const double r = fma(-n, PG_K(1.9082149292705877e-10), fma(-n, PG_K(6.93147180369123816490e-01), x));
+  double p = PG_K(1.6059043836821613e-10);   /* 1/13! */
+  p = fma(p, r, PG_K(2.08767569878681e-09));  /* 1/12! */
+  p = fma(p, r, PG_K(2.505210838544172e-08)); /* 1/11! */
+  p = fma(p, r, PG_K(2.755731922398589e-07)); /* 1/10! */
+  p = fma(p, r, PG_K(2.7557319223985893e-06));
+  p = fma(p, r, PG_K(2.48015873015873e-05));
+  p = fma(p, r, PG_K(1.984126984126984e-04));
+  p = fma(p, r, PG_K(1.388888888888889e-03));
+  p = fma(p, r, PG_K(8.333333333333333e-03));
+  p = fma(p, r, PG_K(4.1666666666666664e-02));
+  p = fma(p, r, PG_K(1.6666666666666666e-01));
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);

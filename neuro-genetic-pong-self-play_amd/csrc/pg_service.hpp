@@ -44,6 +44,9 @@ namespace pg {
 #ifndef PG_INLINE_PRIO
 #define PG_INLINE_PRIO 3
 #endif
+#ifndef PG_INLINE_FRAME_BOUND
+#define PG_INLINE_FRAME_BOUND 1
+#endif
 template <int L, int U, bool kHorizon>
 __host__ __device__ constexpr bool inline_service() {
   return PG_INLINE_SVC && L == 8 && U == 16 && !kHorizon;
@@ -64,24 +67,85 @@ struct InlineReq {
 };
 template <int U, int HL, int O, typename WT>
 __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, InlineReq r, double *lds,
-                                                      int lane64) {
+                                                      int lane64, int stage_base = 0) {
   const int H = p.nodes[1];
   const int b = p.bias;
   float zf[O];
 #pragma unroll
   for (int o = 0; o < O; ++o) zf[o] = r.z[o];
+#ifdef PG_INLINE_LOG  // diagnostic build: one record per request in p.hard_log {z0..z3, e, frame bound, stage | idx << 8, 0}
+  float ef_log = -1.f;
+  const auto log_req = [&](int stage, int idx) {
+    if (p.hard_log && p.counters && lane64 == 0) {
+      const unsigned long long q = atomicAdd((unsigned long long *)&p.counters[9], 1ull);
+      if (q < (unsigned long long)p.hard_cap) {
+        uint32_t *rec = p.hard_log + q * 8;
+        for (int o = 0; o < 4; ++o) rec[o] = __float_as_uint(o < O ? zf[o] : 0.f);
+        rec[4] = __float_as_uint(r.e);
+        rec[5] = __float_as_uint(ef_log);
+        rec[6] = (uint32_t)stage | ((uint32_t)(idx & 255) << 8);
+        rec[7] = 0;
+      }
+    }
+  };
+#define PG_LOG_REQ(stage, idx) log_req(stage, idx)
+#else
+#define PG_LOG_REQ(stage, idx)
+#endif
+#ifdef PG_SERVE_STAGES  // diagnostic build: shader cycles per stage into p.hard_log as u64 sums
+  uint64_t *st_acc = p.hard_log ? (uint64_t *)p.hard_log + stage_base : nullptr;
+  uint64_t st_t = __builtin_amdgcn_s_memtime();
+  const auto stage_mark = [&](int i) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    if (st_acc && lane64 == 0) {
+      atomicAdd((unsigned long long *)&st_acc[i], (unsigned long long)(now - st_t));
+      atomicAdd((unsigned long long *)&st_acc[8 + i], 1ull);
+    }
+    st_t = now;
+  };
+#define PG_STAGE(i) stage_mark(i)
+#else
+#define PG_STAGE(i)
+#endif
   int d = plateau_decide<O>(zf, r.e, lane64);
-  if (d < 0 && r.e < __builtin_inff()) {  // e = inf: weights over the cap, f64 only
+  PG_STAGE(0);
+  if (d >= 0) PG_LOG_REQ(1, d);
+  // the frame's own bound (frame_bound_wave) before the f64 stage: the lane
+  // records' round trip settles ~1/3 of the requests without the genome row's
+  // (PG_INLINE_FRAME_BOUND=0, straight to the f64 stage: the headline -4 %,
+  // --dist init neutral; profiles/r06/ab_tight_fb_c4.log)
+  if (PG_INLINE_FRAME_BOUND && d < 0 && r.e < __builtin_inff()) {  // e = inf: weights over the cap, f64 only
     const float ef = fminf(r.e, frame_bound_wave<HL, U, O>(r.rec, r.kr, lane64));
+#ifdef PG_INLINE_LOG
+    ef_log = ef;
+#endif
+    PG_STAGE(1);
     d = certify_c<O>(zf, make_cert(ef));
     if (d < 0) d = plateau_f32<O>(zf, ef);
     if (d < 0) d = plateau_decide<O>(zf, ef, lane64);
-    if (d >= 0) return d | 1024;
+    PG_STAGE(2);
+    if (d >= 0) {
+      PG_LOG_REQ(2, d);
+      return d | 1024;
+    }
   }
-  if (d < 0) d = fast_f64_decide<O, WT>(g, H, b, r.k, lane64);
+  if (d < 0) {
+    d = fast_f64_decide<O, WT>(g, H, b, r.k, lane64);
+    PG_STAGE(3);
+    if (d >= 0) PG_LOG_REQ(3, d);
+  }
   if (d >= 0) return d | 512;
   d = forward_f64_group<64, (U * HL + 63) / 64, O, WT>(g, H, b, r.k, lds, lane64);
+  PG_LOG_REQ(4, d);
+  PG_STAGE(4);
+#undef PG_LOG_REQ
+#undef PG_STAGE
+#if defined(PG_INLINE_LOG) || defined(PG_SERVE_STAGES)
+  if (false) {
+#else
   if (p.hard_log && lane64 == 0) {
+#endif
     const long oo = g - (const WT *)p.opponents;
     const bool opp = p.opponents != p.genomes && oo >= 0 && oo < (long)p.n_opponents * p.ostride;
     log_hard(p, (int)(opp ? oo / p.ostride : (g - (const WT *)p.genomes) / p.gstride), opp ? 1 : 0, d, 0, r.k);
@@ -503,7 +567,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
       partial_pk<U, O, true>(net, k, acc);
 #pragma unroll
       for (int o = 0; o < O; ++o) z[o] = group_sum<HL>(acc[o]);
-      int code = certify_c8<O>(z, net.ct);  // the decision as 8 x its action code, or -1
+      int code = certify_c8<O>(z, net.ct);  // the decision as its paddle move (index_to_move), or -1
 #ifdef PG_PROBE_EXTRA  // timing-only experiment build: extra instructions of one class every visible frame
       pg_probe_extra<PG_PROBE_EXTRA>(net.w1[0][0], net.w1[1][1], z[0], z[1], probe_v, probe_p, probe_s);
 #endif
@@ -523,10 +587,23 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifdef PG_TIMELINE
         g_fails += 1;
 #endif
-        const int idx = plateau_f32<O>(z, net.e);
-        inwave += idx >= 0 ? 1 : 0;
-        code = idx >= 0 ? index_to_move(idx) : -1;
+        // the gap rule at the plateau's true width (one exp2), else the f32 plateau rule
+#ifndef PG_NO_TIGHT
+        int mv = tight_gap_move<O>(z, net.e, net.ct);
+        if (mv == -1)
+#else
+        int mv = -1;
+#endif
+        {
+          const int idx = plateau_f32<O>(z, net.e);
+          mv = idx >= 0 ? index_to_move(idx) : -1;
+        }
+        inwave += mv != -1 ? 1 : 0;
+        code = mv;
       }
+#ifdef PG_ABLATE_SERVE  // timing-only build: the requests serve_inline would take, decided by a compare
+      if (code == -1) code = z[1] > z[0] ? 6 : -6;
+#endif
       if (kInline && PG_ANY(code == -1)) {
         // the memo, then the whole wave decides each still-undecided half-group in turn
         uint64_t key = 0;
@@ -569,7 +646,12 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           const uint64_t ga = (uint64_t)gm;
           const WT *g = (const WT *)(((uint64_t)__builtin_amdgcn_readlane((int)(ga >> 32), src) << 32) |
                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ga, src));
+#ifdef PG_SERVE_TWICE  // diagnostic: the same request served twice, the second call's stages at +16
+          serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64, 0);
+          const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64, 16);
+#else
           const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64);
+#endif
           if ((lane64 & ~(HL - 1)) == src) {  // the requesting half-group
             slow += (ans >> 8) & 1;
             plateau += (ans >> 9) & 1;
@@ -587,9 +669,26 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
         {
           // the output layer back from the lane records: its registers were
           // the f64 code's (the input layer's stay live across it)
+#if defined(PG_RELOAD_ALL)  // the whole network reloaded: its registers all the f64 code's while it decides
+          load_rec<U, O>(net, p.recs + ((long)slots[sx].rec * HL + hl) * rec_floats<U, O>());
+#elif !defined(PG_NO_RELOAD)  // (PG_NO_RELOAD: every weight kept live across the f64 code)
           load_rec_out<U, O>(net, p.recs + ((long)slots[sx].rec * HL + hl) * rec_floats<U, O>());
+#endif
+#ifndef PG_NO_RELOAD
 #pragma unroll
           for (int o = 0; o < O; ++o) net.c[o] = hl == 0 ? 0.5f * net.c[o] : 0.f;
+#endif
+#ifdef PG_SERVE_STAGES
+          {
+            const uint64_t r0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            const uint64_t r1 = __builtin_amdgcn_s_memtime();
+            if (p.hard_log && lane64 == 0) {
+              atomicAdd((unsigned long long *)&((uint64_t *)p.hard_log)[5], (unsigned long long)(r1 - r0));
+              atomicAdd((unsigned long long *)&((uint64_t *)p.hard_log)[13], 1ull);
+            }
+          }
+#endif
 #ifdef PG_DECIDE_PROBE
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           probe_dec += __builtin_amdgcn_s_memtime() - probe_d0;

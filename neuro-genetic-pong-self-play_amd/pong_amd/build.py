@@ -16,7 +16,7 @@ HEADERS = [os.path.join(CSRC, h) for h in ("pg_device.hpp", "pg_f64math.h", "pg_
 # k_service instantiations took 10 minutes as one unit
 # (object name, source, extra flags)
 UNITS = [("pong_ga", "pong_ga.hip", []), ("pg_wide", "pg_wide.hip", []), ("pg_pixels", "pg_pixels.hip", []),
-         ("pg_hof", "pg_hof.hip", []), ("pg_gen", "pg_gen.hip", [])] + [
+         ("pg_hof", "pg_hof.hip", []), ("pg_gen", "pg_gen.hip", []), ("pg_decide", "pg_decide.hip", [])] + [
     (f"pg_service_more_L{L}_{f}", "pg_service_more.hip",
      [f"-DPG_MORE_L={L}", f"-DPG_MORE_F64={f}"] + (["-DPG_MORE_DISPATCH"] if (L, f) == (8, 1) else []))
     for L in (8, 16, 32, 64) for f in (1, 0)]

@@ -12,7 +12,7 @@ k_service<8,16,3,double,untraced,no-horizon> and reports
   * every scratch (spill) instruction of the kernel by source line: where the
     register allocator spilled, so that none sits on the common path.
 
-    python tools/isa_frame.py [> profiles/r05/isa_frame.txt]
+    python tools/isa_frame.py [-DNAME ...] [--dump listing.txt] [> profiles/r05/isa_frame.txt]
 """
 import collections
 import os
@@ -28,12 +28,12 @@ HIPCC = "/opt/rocm/bin/hipcc"
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
-def disassemble(tmp):
+def disassemble(tmp, defs=()):
     obj = os.path.join(tmp, "k.o")
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                            "-fno-slp-vectorize", "-I", os.path.join(REPO, "include"), "-mllvm",
                            "-amdgpu-sched-strategy=iterative-ilp", "-gline-tables-only", "--cuda-device-only",
-                           "--no-gpu-bundle-output", "-c", "-o", obj, os.path.join(CSRC, "pong_ga.hip")])
+                           "--no-gpu-bundle-output", *defs, "-c", "-o", obj, os.path.join(CSRC, "pong_ga.hip")])
     out = subprocess.check_output([OBJDUMP, "-d", "-l", "--no-show-raw-insn", "--disassemble-symbols=" + SYM, obj],
                                   text=True)
     rows, cur = [], "?"
@@ -73,8 +73,18 @@ def cls(ins):
 
 
 def main():
+    # options: -DNAME... (an experiment build's defines), --dump FILE (the annotated listing)
+    defs = [a for a in sys.argv[1:] if a.startswith("-D")]
+    for i, a in enumerate(sys.argv):  # -mllvm OPTION pairs pass through
+        if a == "-mllvm" and i + 1 < len(sys.argv):
+            defs += [a, sys.argv[i + 1]]
+    dump = sys.argv[sys.argv.index("--dump") + 1] if "--dump" in sys.argv else None
     with tempfile.TemporaryDirectory() as tmp:
-        rows = disassemble(tmp)
+        rows = disassemble(tmp, defs)
+    if dump:
+        with open(dump, "w") as fh:
+            for a, src, ins in rows:
+                fh.write(f"{a:8x}  {src:28s} {ins}\n")
     by_addr = {a: i for i, (a, _, _) in enumerate(rows)}
     # the loop: the last backward conditional branch taken from the `if (top)`
     # test's source line; its fall-through s_branch leads to the common path
