@@ -116,8 +116,14 @@ class DeviceEnv:
         self.game, self.players = int(game), int(players)
         self.use_restricted_actions = None
         self._ph = self._frame = None
+        self._reset_pending = True
 
     def reset(self):
+        # the device state is (re)made by the next step: resetting touches no GPU
+        self._reset_pending = True
+        self._frame = None
+
+    def _device_reset(self):
         from pong_amd import device as D
         from pong_amd import replay
         dev = torch.device(DEVICE)  # noqa: F405
@@ -129,12 +135,12 @@ class DeviceEnv:
         seed = seed - (1 << 64) if seed >= 1 << 63 else seed
         self._ph.reset(torch.tensor([seed], dtype=torch.int64, device=dev),
                        torch.tensor([1 if self.players == 1 else 0], dtype=torch.int32, device=dev))
-        self._frame = None
+        self._reset_pending = False
 
     def step(self, action):
         from pong_amd import device as D
-        if self._ph is None:
-            self.reset()
+        if self._ph is None or self._reset_pending:
+            self._device_reset()
         a = [int(v) for v in action]
         bits = a[4] | (a[5] << 1) | (a[6] << 2) | (a[7] << 3)
         self._ph.step(torch.tensor([bits], dtype=torch.uint8, device=self._ph.device))
