@@ -943,15 +943,19 @@ __device__ __forceinline__ void f64_features(const int *k, double *x) {
 }
 
 // fast_f64_decide's decision from the lanes' partial output sums zp and bound
-// sums ep (any lane order: e covers it) and the output biases c.
+// sums ep (any lane order: e covers it) and the output biases c.  The bound's
+// sum runs in f32 (a bound only needs to stay above its true value: 64 positive
+// terms in f32 are within 64 2^-24 < 4e-6 of their exact sum, covered by the
+// x1.001 margin below; each term is rounded up by 1 + 2^-22 first), one DPP
+// f32 reduction instead of an f64 one of twice the moves.
 template <int O>
-__device__ int f64_decide_sums(const double *zp, const double *ep, const double *c, int lane) {
+__device__ int f64_decide_sums(const double *zp, const float *ep, const double *c, int lane) {
   constexpr double kEps = 1.1102230246251565e-16;  // 2^-53
   double z[O], e[O];
 #pragma unroll
   for (int o = 0; o < O; ++o) {
     const double t = wave_sum_f64(zp[o]);
-    const double u = wave_sum_f64(ep[o]);
+    const double u = (double)group_sum<64>(ep[o] * 1.00000024f);
     z[o] = t + c[o];
     e[o] = 2.0 * kEps * (u + 2.0 * fabs(c[o])) * PG_K(1.001) + PG_K(1e-300);
   }
@@ -1024,9 +1028,10 @@ __device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int
   f64_features(k, x);
   const int cols = 6 + b;
   const WT *v = g + (long)H * cols;
-  double zp[O], ep[O], c[O];
+  double zp[O], c[O];
+  float ep[O];
 #pragma unroll
-  for (int o = 0; o < O; ++o) { zp[o] = 0.0; ep[o] = 0.0; }
+  for (int o = 0; o < O; ++o) { zp[o] = 0.0; ep[o] = 0.f; }
 #pragma unroll 1
   for (int j = lane; j < H; j += 64) {
     const WT *row = g + (long)j * cols;
@@ -1039,7 +1044,8 @@ __device__ int fast_f64_decide(const WT *__restrict__ g, int H, int b, const int
     for (int o = 0; o < O; ++o) {
       const double w2 = (double)v[(long)o * (H + b) + j];
       zp[o] = fma(w2, sj, zp[o]);
-      ep[o] = fma(fabs(w2), aj, ep[o]);
+      // |w2| aj rounded up to f32 (x 1.00000024 = 1 + 2^-22: above one f32 rounding of each of the two)
+      ep[o] = fmaf((float)(fabs(w2) * aj), 1.00000024f, ep[o]);
     }
   }
 #pragma unroll
@@ -1080,11 +1086,12 @@ __device__ __forceinline__ void fast_f64_decide_batch(const WT *const *g, const 
       f64_features(k[q], x);
       double sj, aj;
       f64_unit(x, w1[q], b, sj, aj);
-      double zp[O], ep[O];
+      double zp[O];
+      float ep[O];
 #pragma unroll
       for (int o = 0; o < O; ++o) {
         zp[o] = on ? w2[q][o] * sj : 0.0;
-        ep[o] = on ? fabs(w2[q][o]) * aj : 0.0;
+        ep[o] = on ? (float)(fabs(w2[q][o]) * aj) * 1.00000024f : 0.f;
       }
       out[q] = f64_decide_sums<O>(zp, ep, c[q], lane);
     }

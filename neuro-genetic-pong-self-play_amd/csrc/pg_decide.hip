@@ -83,7 +83,8 @@ __global__ __launch_bounds__(64) void k_decide(DecideParams p) {
       float zf[O];
 #pragma unroll
       for (int o = 0; o < O; ++o) zf[o] = zs[q][o];
-      int idx = plateau_decide<O>(zf, es[q], lane);
+      // serve_inline's order: with the frame bound, no plateau rule under the static one first
+      int idx = kFrameBound ? -1 : plateau_decide<O>(zf, es[q], lane);
       int st = 2;
       if constexpr (kFrameBound) {
         if (idx < 0 && es[q] < __builtin_inff()) {  // serve_inline's order

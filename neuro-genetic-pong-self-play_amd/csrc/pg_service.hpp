@@ -47,9 +47,14 @@ namespace pg {
 #ifndef PG_INLINE_FRAME_BOUND
 #define PG_INLINE_FRAME_BOUND 1
 #endif
+// The fixed-horizon instance too since round 6 (PG_HORIZON_INLINE=0: its
+// service wave, as round 5's).
+#ifndef PG_HORIZON_INLINE
+#define PG_HORIZON_INLINE 1
+#endif
 template <int L, int U, bool kHorizon>
 __host__ __device__ constexpr bool inline_service() {
-  return PG_INLINE_SVC && L == 8 && U == 16 && !kHorizon;
+  return PG_INLINE_SVC && L == 8 && U == 16 && (PG_HORIZON_INLINE || !kHorizon);
 }
 
 // One request, by the whole wave (every lane active): the f32 outputs'
@@ -67,7 +72,7 @@ struct InlineReq {
 };
 template <int U, int HL, int O, typename WT>
 __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, InlineReq r, double *lds,
-                                                      int lane64, int stage_base = 0) {
+                                                      int lane64, uint64_t *st_acc = nullptr) {
   const int H = p.nodes[1];
   const int b = p.bias;
   float zf[O];
@@ -92,23 +97,26 @@ __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, In
 #else
 #define PG_LOG_REQ(stage, idx)
 #endif
-#ifdef PG_SERVE_STAGES  // diagnostic build: shader cycles per stage into p.hard_log as u64 sums
-  uint64_t *st_acc = p.hard_log ? (uint64_t *)p.hard_log + stage_base : nullptr;
+#ifdef PG_SERVE_STAGES  // diagnostic build: shader cycles per stage, summed in the wave's st_acc[0..11]
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   uint64_t st_t = __builtin_amdgcn_s_memtime();
   const auto stage_mark = [&](int i) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     const uint64_t now = __builtin_amdgcn_s_memtime();
-    if (st_acc && lane64 == 0) {
-      atomicAdd((unsigned long long *)&st_acc[i], (unsigned long long)(now - st_t));
-      atomicAdd((unsigned long long *)&st_acc[8 + i], 1ull);
-    }
+    st_acc[i] += now - st_t;
+    st_acc[6 + i] += 1;
     st_t = now;
   };
 #define PG_STAGE(i) stage_mark(i)
 #else
 #define PG_STAGE(i)
 #endif
-  int d = plateau_decide<O>(zf, r.e, lane64);
+  // the plateau rule under the network's static bound first only where the
+  // frame bound does not follow (PG_INLINE_FRAME_BOUND=0): under the frame's
+  // bound the same rule decides everything it would (round 6: it settled
+  // 0.1 % of the bench's requests and 15 % of --dist init's, at ~2k cycles
+  // each; profiles/r06/serve_stages_c10.log)
+  int d = PG_INLINE_FRAME_BOUND ? -1 : plateau_decide<O>(zf, r.e, lane64);
   PG_STAGE(0);
   if (d >= 0) PG_LOG_REQ(1, d);
   // the frame's own bound (frame_bound_wave) before the f64 stage: the lane
@@ -414,6 +422,7 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
     st.one_player = 0;
     kind = kOppNN;
     tend = 0x7fffffff;
+    fstart = 0x3fffffff;  // (the fixed-horizon end test sframe - fstart >= T never fires either)
     fresh = false;
   };
   if (kInline && !live) park();
@@ -432,6 +441,11 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #ifdef PG_START_PROBE  // diagnostic build: shader cycles of the game-start blocks vs the wave's total
   uint64_t probe_fresh = 0;
   const uint64_t probe_t0 = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef PG_SERVE_STAGES  // diagnostic build: serve_inline's cycles per stage (and a second call's, PG_SERVE_TWICE)
+  uint64_t st_acc[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) st_acc[i] = 0;
 #endif
 #ifdef PG_DECIDE_PROBE  // diagnostic build: shader cycles of kInline's f64 decisions (until the reload has landed) vs the wave's total
   uint64_t probe_dec = 0;
@@ -646,9 +660,11 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           const uint64_t ga = (uint64_t)gm;
           const WT *g = (const WT *)(((uint64_t)__builtin_amdgcn_readlane((int)(ga >> 32), src) << 32) |
                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ga, src));
-#ifdef PG_SERVE_TWICE  // diagnostic: the same request served twice, the second call's stages at +16
-          serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64, 0);
-          const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64, 16);
+#if defined(PG_SERVE_TWICE)  // diagnostic: the same request served twice, the second call's stages at +12
+          serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64, st_acc);
+          const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64, st_acc + 12);
+#elif defined(PG_SERVE_STAGES)
+          const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64, st_acc);
 #else
           const int ans = serve_inline<U, HL, O, WT>(p, g, r, lds_svc + wave * f64_lds_doubles(H, O), lane64);
 #endif
@@ -682,11 +698,8 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
           {
             const uint64_t r0 = __builtin_amdgcn_s_memtime();
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            const uint64_t r1 = __builtin_amdgcn_s_memtime();
-            if (p.hard_log && lane64 == 0) {
-              atomicAdd((unsigned long long *)&((uint64_t *)p.hard_log)[5], (unsigned long long)(r1 - r0));
-              atomicAdd((unsigned long long *)&((uint64_t *)p.hard_log)[13], 1ull);
-            }
+            st_acc[5] += __builtin_amdgcn_s_memtime() - r0;
+            st_acc[11] += 1;
           }
 #endif
 #ifdef PG_DECIDE_PROBE
@@ -949,6 +962,12 @@ __global__ __launch_bounds__(svc_threads<U>()) void k_service(EvalParams p) {
 #endif
 #ifdef PG_PROBE_EXTRA  // keep the probe's results alive (never true)
   if (p.counters && probe_v == 1234.5f && probe_p.x == 1234.5f && probe_s == 1234567) p.counters[15] = 1;
+#endif
+#ifdef PG_SERVE_STAGES
+  if (p.hard_log && lane64 == 0)
+#pragma unroll
+    for (int i = 0; i < 24; ++i)
+      if (st_acc[i]) atomicAdd((unsigned long long *)&((uint64_t *)p.hard_log)[i], (unsigned long long)st_acc[i]);
 #endif
   // this wave will post no more requests
   if (lane64 == 0) atomicAdd(&waves_done, 1);

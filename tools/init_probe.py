@@ -27,12 +27,12 @@ def stages(ga, dev):
     acc = ga.hard_log.cpu().numpy().view(np.uint64).reshape(-1)
     names = ["plateau_decide (static e)", "frame bound (records + 64-lane sums)", "rules under the frame bound",
              "fast_f64_decide (genome + f64)", "numpy-order forward", "output layer reload wait"]
-    for base, what in ((0, "first call"), (16, "the same request again (PG_SERVE_TWICE)")):
-        if not acc[base + 8:base + 14].any():
+    for base, what in ((0, "first call"), (12, "the same request again (PG_SERVE_TWICE)")):
+        if not acc[base + 6:base + 12].any():
             continue
         print(what)
         for i, nm in enumerate(names):
-            n = int(acc[base + 8 + i])
+            n = int(acc[base + 6 + i])
             if n:
                 print(f"  {nm:40s} calls {n:9d}  mean cycles {acc[base + i] / n:9.0f}  total {acc[base + i] / 1e9:7.2f} G")
 
