@@ -41,6 +41,7 @@
  * pg_hof_rank_classes            their hashes, the (fitness, age) ranks and
  *                                similarity classes the host scan reads
  * pg_hof_update (host)           tools.HallOfFame.update (eaSimple, main.py:165-170)
+ * pg_hof_update_packed (host)    the same over the device's packed ranks and classes, O(k log k)
  * pg_gather_rows                 the new hall's genomes (HallOfFame.insert's deepcopy)
  * pg_ga_scatter_fitness /        eaSimple's bookkeeping around toolbox.map
  * pg_ga_merge_fitness            (main.py:165-170): fitness assigned to invalid_ind,
@@ -388,6 +389,28 @@ typedef struct pg_hof_args {
                                     hof_n + i = population row i */
   double *new_fitness;           /* out [maxsize] */
 } pg_hof_args;
+
+/* pg_hof_update over the device's packing (pg_hof_rank_classes /
+ * pg_hof_prepare_cand: packed[e] = rank | class << 32 for the hof_n members in
+ * items order and the k candidates in population order, then the candidates'
+ * fitness bits), host arrays.  The same rule and result as pg_hof_update, in
+ * O(k log k + new_n): the members are in items order, so the worst remaining
+ * member is always the last not yet evicted, and a member class (the first
+ * member of its hash) is present exactly while that member is; only the
+ * members at the hall's tail and the candidates are visited, and the output
+ * is filled by ranges.  Falls back to the full scan when the members' ranks
+ * are not descending. */
+typedef struct pg_hof_packed_args {
+  int32_t maxsize;               /* HALL_OF_FAME_AMOUNT */
+  int32_t hof_n;                 /* current members */
+  const double *hof_fitness;     /* [hof_n] host, items order */
+  int32_t k;                     /* candidates */
+  const int64_t *packed;         /* [hof_n + 2k] host */
+  int32_t *new_n;                /* out */
+  int32_t *new_src;              /* out [maxsize]: j' < hof_n old member j', hof_n + c candidate c */
+  double *new_fitness;           /* out [maxsize] */
+} pg_hof_packed_args;
+int32_t pg_hof_update_packed(const pg_hof_packed_args *args);
 
 /* Device half of the hall-of-fame update (pg_hof_rank_classes): for the old
  * members (items order) and k candidate rows, each entry's pg_hof_args.rank and

@@ -25,6 +25,7 @@
 #include <cstring>
 #include <string>
 #include <algorithm>
+#include <memory>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -1232,6 +1233,132 @@ int32_t pg_hof_update(const pg_hof_args *a) {
       ++j;
     }
   }
+  *a->new_n = j;
+  return PG_OK;
+}
+
+int32_t pg_hof_update_packed(const pg_hof_packed_args *a) {
+  if (!a) return fail(PG_ERR_INVALID, "args is NULL");
+  const int hn = a->hof_n, k = a->k;
+  if (a->maxsize < 0 || hn < 0 || hn > a->maxsize || k < 0 || !a->new_n || (a->maxsize > 0 && (!a->new_src || !a->new_fitness)) ||
+      (hn > 0 && !a->hof_fitness) || (hn + k > 0 && !a->packed))
+    return fail(PG_ERR_INVALID, "hof_update_packed: bad sizes or NULL buffers");
+  const int64_t *pk = a->packed;
+  const int n = hn + k;
+  auto rank_of = [&](int e) { return (int32_t)(uint32_t)pk[e]; };
+  auto class_of = [&](int e) { return (int32_t)(pk[e] >> 32); };
+  auto cand_fit = [&](int c) {
+    double f;
+    std::memcpy(&f, &pk[n + c], sizeof(double));
+    return f;
+  };
+  // the general scan: the packing decoded (an empty hall's first entrant, or
+  // members whose ranks are not descending)
+  const auto general = [&]() -> int32_t {
+    std::vector<int32_t> rank((size_t)n);
+    std::vector<uint64_t> hh((size_t)hn), ph((size_t)k);
+    std::vector<double> pf((size_t)k);
+    for (int e = 0; e < n; ++e) {
+      rank[e] = rank_of(e);
+      if (e < hn) hh[e] = (uint64_t)class_of(e);
+      else ph[e - hn] = (uint64_t)class_of(e);
+    }
+    for (int c = 0; c < k; ++c) pf[c] = cand_fit(c);
+    pg_hof_args g;
+    g.maxsize = a->maxsize;
+    g.hof_n = hn;
+    g.hof_fitness = a->hof_fitness;
+    g.hof_hash = hh.data();
+    g.pop_n = k;
+    g.pop_fitness = pf.data();
+    g.pop_hash = ph.data();
+    g.rank = rank.data();
+    g.new_n = a->new_n;
+    g.new_src = a->new_src;
+    g.new_fitness = a->new_fitness;
+    return pg_hof_update(&g);
+  };
+  if (a->maxsize == 0) {
+    *a->new_n = 0;
+    return PG_OK;
+  }
+  if (hn == 0) return general();
+  for (int e = 1; e < hn; ++e)
+    if (rank_of(e) >= rank_of(e - 1)) return general();  // members not in items order
+  for (int c = 0; c < k; ++c)
+    if (class_of(hn + c) < 0 || class_of(hn + c) >= n) return fail(PG_ERR_INVALID, "hof_update_packed: class out of range");
+  // accepted candidates present in the hall: a bitmap over the entries'
+  // ranks (cmin = its lowest set bit) and rank -> candidate; their classes'
+  // counts (candidate classes are >= hn)
+  std::vector<uint64_t> cbits(((size_t)n + 63) / 64, 0);
+  std::unique_ptr<int32_t[]> cand_at(new int32_t[(size_t)n]);  // read only where a bit is set
+  int cmin = n;
+  std::vector<int32_t> ccount((size_t)k, 0);
+  // accepted candidates whose class is a member's (their row equals a member
+  // evicted before them): rare, so a small map instead of an array of hof_n
+  std::unordered_map<int32_t, int32_t> mcount;
+  int p = hn - 1;  // members 0..p present: eviction takes the tail first
+  int size = hn;
+  for (int c = 0; c < k; ++c) {
+    const double f = cand_fit(c);
+    const int cls = class_of(hn + c);
+    // the worst present entry: the tail member or the lowest-ranked accepted candidate
+    const bool cand_worst = cmin < n && (p < 0 || cmin < rank_of(p));
+    if (size >= a->maxsize) {  // ind.fitness > self[-1].fitness
+      const double fw = cand_worst ? cand_fit(cand_at[cmin]) : a->hof_fitness[p];
+      if (!(f > fw)) continue;
+    }
+    if (cls < hn ? (cls <= p || mcount.count(cls) > 0) : ccount[cls - hn] > 0) continue;  // similar to a present entry
+    if (size >= a->maxsize) {  // remove(-1)
+      if (cand_worst) {
+        const int wc = class_of(hn + cand_at[cmin]);
+        if (wc >= hn) {
+          ccount[wc - hn] -= 1;
+        } else if (--mcount[wc] == 0) {
+          mcount.erase(wc);
+        }
+        cbits[(size_t)cmin >> 6] &= ~(1ull << (cmin & 63));
+        size_t wd = (size_t)cmin >> 6;
+        uint64_t bits = cbits[wd];
+        while (!bits && ++wd < cbits.size()) bits = cbits[wd];
+        cmin = bits ? (int)(wd * 64 + __builtin_ctzll(bits)) : n;
+      } else {
+        p -= 1;
+      }
+      size -= 1;
+    }
+    const int r = rank_of(hn + c);
+    cbits[(size_t)r >> 6] |= 1ull << (r & 63);
+    cand_at[r] = c;
+    cmin = r < cmin ? r : cmin;
+    if (cls >= hn) ccount[cls - hn] += 1;
+    else mcount[cls] += 1;
+    size += 1;
+  }
+  // items order: members 0..p (descending rank) merged with the present
+  // candidates by descending rank (the bitmap walked down), member runs
+  // copied as ranges
+  int j = 0, m = 0;  // output position, next member
+  for (size_t wd = cbits.size(); wd-- > 0;) {
+    uint64_t bits = cbits[wd];
+    while (bits) {
+      const int hi = 63 - __builtin_clzll(bits);
+      bits &= ~(1ull << hi);
+      const int r = (int)(wd * 64 + hi), c = cand_at[r];
+      int lo = m;  // the members ranked above this candidate
+      while (lo <= p && rank_of(lo) > r) ++lo;
+      for (int e = m; e < lo; ++e) a->new_src[j + e - m] = e;
+      std::memcpy(a->new_fitness + j, a->hof_fitness + m, sizeof(double) * (size_t)(lo - m));
+      j += lo - m;
+      m = lo;
+      a->new_src[j] = hn + c;
+      a->new_fitness[j] = cand_fit(c);
+      ++j;
+    }
+  }
+  for (int e = m; e <= p; ++e) a->new_src[j + e - m] = e;
+  if (p + 1 > m) std::memcpy(a->new_fitness + j, a->hof_fitness + m, sizeof(double) * (size_t)(p + 1 - m));
+  j += p + 1 - m;
   *a->new_n = j;
   return PG_OK;
 }

@@ -117,6 +117,11 @@ class PgScheduleArgs(ctypes.Structure):
     ]
 
 
+class PgHofPackedArgs(ctypes.Structure):
+    _fields_ = [("maxsize", ctypes.c_int32), ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("k", ctypes.c_int32),
+                ("packed", _vp), ("new_n", _vp), ("new_src", _vp), ("new_fitness", _vp)]
+
+
 class PgHofArgs(ctypes.Structure):
     _fields_ = [
         ("maxsize", ctypes.c_int32), ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("hof_hash", _vp),
@@ -202,6 +207,7 @@ SIGNATURES = {
     "pg_row_hash": (ctypes.c_int32, [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _vp,
                                      _vp]),
     "pg_hof_update": (ctypes.c_int32, [ctypes.POINTER(PgHofArgs)]),
+    "pg_hof_update_packed": (ctypes.c_int32, [ctypes.POINTER(PgHofPackedArgs)]),
     "pg_hof_rank_classes_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "pg_hof_rank_classes": (ctypes.c_int32, [ctypes.POINTER(PgHofRankArgs), _vp]),
     "pg_hof_prepare_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),

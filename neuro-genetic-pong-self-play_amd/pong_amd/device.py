@@ -610,6 +610,25 @@ def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash, rank=
     return src[: new_n.value].copy(), fit[: new_n.value].copy()
 
 
+def hof_update_packed(maxsize: int, hof_fitness, packed, k: int):
+    """pg_hof_update_packed (host, no GPU): HallOfFame.update from the device's
+    packing (pg_hof_prepare_cand: rank | class << 32 per member then per
+    candidate, then the candidates' fitness bits); returns (src, fitness) as
+    hof_update does."""
+    import numpy as np
+    hf = np.ascontiguousarray(hof_fitness, dtype=np.float64)
+    pk = np.ascontiguousarray(packed, dtype=np.int64)
+    if pk.shape[0] < hf.shape[0] + 2 * k:
+        raise ValueError("packed must hold hof_n + 2k entries")
+    src = np.empty(max(maxsize, 1), dtype=np.int32)
+    fit = np.empty(max(maxsize, 1), dtype=np.float64)
+    new_n = ctypes.c_int32(0)
+    a = L.PgHofPackedArgs(maxsize, hf.shape[0], hf.ctypes.data, int(k), pk.ctypes.data, ctypes.addressof(new_n),
+                          src.ctypes.data, fit.ctypes.data)
+    L.check("pg_hof_update_packed", L.lib().pg_hof_update_packed(ctypes.byref(a)))
+    return src[: new_n.value], fit[: new_n.value]
+
+
 FRAME_SHAPE = (210, 160, 3)  # obs.npy
 
 

@@ -750,11 +750,9 @@ class DeviceGA:
             overlap()
             self._mark("next_select_vary", sub=True)
         copied.synchronize()
-        pk = packed_h.numpy()
-        rank_np = (pk[:n] & 0xFFFFFFFF).astype(np.int32)
-        cls_np = pk[:n] >> 32
-        src, new_fit = D.hof_update(self.H, self._hof_fit_host, cls_np[:old_n], pk[n:].view(np.float64),
-                                    cls_np[old_n:], rank=rank_np)
+        # the scan straight on the device's packing, visiting only the hall's
+        # tail and the candidates (pg_hof_update_packed, O(k log k))
+        src, new_fit = D.hof_update_packed(self.H, self._hof_fit_host, packed_h.numpy(), k)
         self._mark("hof_scan", sub=True)
         m = src.shape[0]
         up = torch.empty(3 * m, dtype=torch.int32, pin_memory=True)

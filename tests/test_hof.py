@@ -136,3 +136,78 @@ def test_hof_update_general_path_unordered_members():
     assert list(fit_u) == list(fit_o)
     back = np.array([perm[s] if s < H else s for s in src_o])
     assert list(src_u) == list(back)
+
+
+def _packing(keys_f, keys_h, fit, hsh):
+    """pg_hof_prepare_cand's packing in numpy: ranks in ascending (fitness, age)
+    order, dense classes (a member's: the first member of equal hash; a
+    candidate's: that member, else hof_n + the first candidate of equal hash),
+    then the candidates' fitness bits."""
+    hn, k = len(keys_f), len(fit)
+    rank = _ranks(keys_f, fit).astype(np.int64)
+    first_m, cls = {}, np.empty(hn + k, np.int64)
+    for e in range(hn):
+        cls[e] = first_m.setdefault(int(keys_h[e]), e)
+    first_c = {}
+    for c in range(k):
+        h = int(hsh[c])
+        cls[hn + c] = first_m[h] if h in first_m else first_c.setdefault(h, hn + c)
+    return np.concatenate([rank | (cls << 32), np.asarray(fit, np.float64).view(np.int64)])
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_hof_update_packed_matches_deap(Ind, seed):
+    """pg_hof_update_packed (the O(k log k) scan DeviceGA uses) against DEAP's
+    HallOfFame over successive generations: full and filling halls, ties,
+    duplicates among candidates and with members."""
+    rng = np.random.default_rng(2000 + seed)
+    maxsize = int(rng.integers(1, 300))
+    hof = tools.HallOfFame(maxsize)
+    keys_f, keys_h = np.zeros(0), np.zeros(0, np.int64)
+    genes = rng.integers(-2**62, 2**62, size=int(rng.integers(2, 400)))
+    for _ in range(5):
+        n = int(rng.integers(0, 600))
+        fit = np.round(rng.standard_normal(n) * 2, int(rng.integers(0, 3)))
+        hsh = genes[rng.integers(0, genes.size, size=n)]
+        hof.update([_mk(Ind, h, f) for h, f in zip(hsh, fit)])
+        src, new_fit = D.hof_update_packed(maxsize, keys_f, _packing(keys_f, keys_h, fit, hsh), n)
+        old_n = keys_f.shape[0]
+        new_h = np.array([keys_h[s] if s < old_n else hsh[s - old_n] for s in src], dtype=np.int64)
+        assert [i.fitness.values[0] for i in hof] == list(new_fit)
+        assert [i[0] for i in hof] == list(new_h)
+        keys_f, keys_h = new_fit.copy(), new_h
+
+
+def test_hof_update_packed_equals_general_large():
+    """At BASELINE config 4's sizes (a 131 072-member hall, ~18 700 candidates
+    above its worst) the packed scan returns pg_hof_update's result exactly."""
+    rng = np.random.default_rng(9)
+    H, k = 131072, 18721
+    hof_f = np.sort(rng.normal(size=H))[::-1].copy()
+    hof_h = rng.integers(-2**62, 2**62, size=H)
+    fit = rng.normal(size=k) + 2.0
+    hsh = rng.integers(-2**62, 2**62, size=k)
+    hsh[::17] = hof_h[rng.integers(0, H, size=hsh[::17].size)]  # similar to members
+    hsh[5::23] = hsh[rng.integers(0, k, size=hsh[5::23].size)]  # similar to other candidates
+    packed = _packing(hof_f, hof_h, fit, hsh)
+    src_p, fit_p = D.hof_update_packed(H, hof_f, packed, k)
+    cls = packed[:H + k] >> 32
+    src_g, fit_g = D.hof_update(H, hof_f, cls[:H], fit, cls[H:], rank=(packed[:H + k] & 0xFFFFFFFF).astype(np.int32))
+    np.testing.assert_array_equal(src_p, src_g)
+    np.testing.assert_array_equal(fit_p, fit_g)
+
+
+def test_hof_update_packed_unordered_members_fall_back():
+    rng = np.random.default_rng(3)
+    H = 32
+    mf = rng.permutation(np.arange(H, dtype=np.float64))
+    mh = rng.integers(-2**62, 2**62, size=H)
+    pf = rng.standard_normal(50) * 20 + 20
+    ph = rng.integers(-2**62, 2**62, size=50)
+    # ranks as the device would give them for these (unordered) members
+    packed = _packing(mf, mh, pf, ph)
+    src_p, fit_p = D.hof_update_packed(H, mf, packed, 50)
+    cls = packed[:H + 50] >> 32
+    src_g, fit_g = D.hof_update(H, mf, cls[:H], pf, cls[H:], rank=(packed[:H + 50] & 0xFFFFFFFF).astype(np.int32))
+    np.testing.assert_array_equal(src_p, src_g)
+    np.testing.assert_array_equal(fit_p, fit_g)
