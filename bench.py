@@ -47,7 +47,7 @@ import torch.distributed as dist  # noqa: E402
 
 F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
-PROFILE_ROUND = "r05"           # profiles/<round>/ holds the PMC passes of the committed build
+PROFILE_ROUND = "r06"           # profiles/<round>/ holds the PMC passes of the committed build
 
 
 def parse():
@@ -145,9 +145,11 @@ def main():
     ga.ev.horizon = args.horizon  # pg_eval_args.horizon: 0 = evaluate()'s episodes
     ga.order_by_length = os.environ.get("PG_NO_LENGTH_ORDER") != "1"  # A/B switch for the evaluation order
     ga.early_prep = os.environ.get("PG_NO_EARLY_PREP") != "1"  # A/B switch: schedule + genome records during the HoF scan
-    # config 5 (strong scaling): each rank plays an equal share of long and short
-    # genomes, dealt by predicted game length (DeviceGA.balance_shards; N > 1 only)
-    ga.balance_shards = args.config == "wide" and os.environ.get("PG_NO_BALANCE") != "1"
+    # config 5 (strong scaling): contiguous shards.  Length-balanced shards
+    # (DeviceGA.balance_shards, PG_BALANCE=1) measured no better at P = 65 536:
+    # 8 192 genomes a rank already even out (straggler factor 1.0016 contiguous
+    # vs 1.0069 balanced at N = 8; profiles/r06/scale_model_wide.log)
+    ga.balance_shards = args.config == "wide" and os.environ.get("PG_BALANCE") == "1"
     G = ga.G
     ga.initialize("normal" if args.dist == "normal" else "uniform", args.sigma)
     # the first games already face a full hall of fame: H independent random

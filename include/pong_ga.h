@@ -67,7 +67,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 11
+#define PG_ABI_VERSION 12
 #define PG_MAX_NODES 9 /* len(NETWORK_SHAPE) <= 9 */
 
 typedef enum pg_status {
@@ -409,6 +409,14 @@ typedef struct pg_hof_packed_args {
   int32_t *new_n;                /* out */
   int32_t *new_src;              /* out [maxsize]: j' < hof_n old member j', hof_n + c candidate c */
   double *new_fitness;           /* out [maxsize] */
+  /* ABI 12, the hall kept in place: member j's row lives in storage slot
+   * slot[j].  slot_in [hof_n] (NULL: slot j = j) the members' slots; slot_out
+   * (NULL: not computed) [maxsize] out: a kept member keeps its slot, an
+   * entering candidate takes a slot an evicted member freed (in items order
+   * of the evicted) or, while the hall grows, slot hof_n, hof_n + 1, ...;
+   * the slots in use are always [0, new_n). */
+  const int32_t *slot_in;
+  int32_t *slot_out;
 } pg_hof_packed_args;
 int32_t pg_hof_update_packed(const pg_hof_packed_args *args);
 
@@ -621,6 +629,12 @@ typedef struct pg_hof_commit_args {
   uint64_t *new_hash;            /* out [m] */
   const double *fitness_in;      /* [m] device */
   double *new_fitness;           /* out [m] */
+  /* ABI 12: dst_slot [m] device (NULL: member j's row is dst row j).  Non-NULL:
+   * the hall in place -- dst is the hall's storage, member j's row is dst row
+   * dst_slot[j] (pg_hof_packed_args.slot_out), and only entering candidates'
+   * rows are written (a kept member's row is already in its slot; old_rows is
+   * not read).  Hashes and fitness are written by position as without it. */
+  const int32_t *dst_slot;
 } pg_hof_commit_args;
 int32_t pg_hof_commit(const pg_hof_commit_args *args, void *stream);
 

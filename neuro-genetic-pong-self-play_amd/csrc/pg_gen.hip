@@ -342,12 +342,16 @@ __global__ __launch_bounds__(256) void k_hof_commit(WT *dst, int64_t dst_stride,
                                                     const WT *rows, int64_t rows_stride, const int32_t *cand,
                                                     const int32_t *src, int n_old, int64_t genes,
                                                     const uint64_t *old_hash, const uint64_t *cand_hash,
-                                                    uint64_t *new_hash, const double *fit_in, double *new_fitness) {
+                                                    uint64_t *new_hash, const double *fit_in, double *new_fitness,
+                                                    const int32_t *dst_slot) {
   const int j = blockIdx.x;
   const int s = src[j];
-  const WT *from = s < n_old ? old_rows + (long)s * old_stride : rows + (long)cand[s - n_old] * rows_stride;
-  WT *to = dst + (long)j * dst_stride;
-  for (int64_t g = threadIdx.x; g < genes; g += 256) to[g] = from[g];
+  // (dst_slot: the hall in place -- a kept member's row is already in its slot)
+  if (!dst_slot || s >= n_old) {
+    const WT *from = s < n_old ? old_rows + (long)s * old_stride : rows + (long)cand[s - n_old] * rows_stride;
+    WT *to = dst + (long)(dst_slot ? dst_slot[j] : j) * dst_stride;
+    for (int64_t g = threadIdx.x; g < genes; g += 256) to[g] = from[g];
+  }
   if (threadIdx.x == 0) {
     new_hash[j] = s < n_old ? old_hash[s] : cand_hash[s - n_old];
     new_fitness[j] = fit_in[j];
@@ -516,7 +520,7 @@ int32_t pg_hof_commit(const pg_hof_commit_args *a, void *stream) {
   if (!a) return fail(PG_ERR_INVALID, "args is NULL");
   if (a->m < 0 || a->n_old < 0 || a->genes < 0 || (a->dtype != PG_F32 && a->dtype != PG_F64) ||
       (a->m > 0 && (!a->dst || !a->src || !a->new_hash || !a->fitness_in || !a->new_fitness)) ||
-      (a->m > 0 && a->n_old > 0 && (!a->old_rows || !a->old_hash)) ||
+      (a->m > 0 && a->n_old > 0 && ((!a->old_rows && !a->dst_slot) || !a->old_hash)) ||
       (a->m > 0 && (!a->rows || !a->cand || !a->cand_hash)))
     return fail(PG_ERR_INVALID, "hof_commit: bad sizes, dtype or NULL buffers");
   if (a->m == 0) return PG_OK;
@@ -525,12 +529,12 @@ int32_t pg_hof_commit(const pg_hof_commit_args *a, void *stream) {
     hipLaunchKernelGGL(k_hof_commit<double>, dim3(a->m), dim3(256), 0, s, (double *)a->dst, a->dst_stride,
                        (const double *)a->old_rows, a->old_stride, (const double *)a->rows, a->rows_stride, a->cand,
                        a->src, a->n_old, a->genes, a->old_hash, a->cand_hash,
-                       a->new_hash, a->fitness_in, a->new_fitness);
+                       a->new_hash, a->fitness_in, a->new_fitness, a->dst_slot);
   else
     hipLaunchKernelGGL(k_hof_commit<float>, dim3(a->m), dim3(256), 0, s, (float *)a->dst, a->dst_stride,
                        (const float *)a->old_rows, a->old_stride, (const float *)a->rows, a->rows_stride, a->cand,
                        a->src, a->n_old, a->genes, a->old_hash, a->cand_hash,
-                       a->new_hash, a->fitness_in, a->new_fitness);
+                       a->new_hash, a->fitness_in, a->new_fitness, a->dst_slot);
   PG_HIP(hipGetLastError());
   return PG_OK;
 }

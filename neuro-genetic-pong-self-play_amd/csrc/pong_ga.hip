@@ -1237,12 +1237,45 @@ int32_t pg_hof_update(const pg_hof_args *a) {
   return PG_OK;
 }
 
+namespace {
+// The hall in place (pg_hof_packed_args.slot_out), for the general scan's
+// result: kept members keep their slots; entering candidates take the freed
+// slots -- those of the members not kept, in items order, then hof_n,
+// hof_n + 1, ... -- in output order (the packed scan does the same inline).
+int32_t assign_slots(int hn, int new_n, const int32_t *slot_in, const int32_t *src, int32_t *slot_out) {
+  const auto slot_of = [&](int e) { return slot_in ? slot_in[e] : e; };
+  std::vector<int32_t> freed;
+  std::vector<uint8_t> kept((size_t)hn, 0);
+  for (int j = 0; j < new_n; ++j)
+    if (src[j] < hn) kept[src[j]] = 1;
+  for (int e = 0; e < hn; ++e)
+    if (!kept[e]) freed.push_back(slot_of(e));
+  size_t next = 0;
+  int grow = hn;
+  for (int j = 0; j < new_n; ++j) {
+    if (src[j] < hn) {
+      slot_out[j] = slot_of(src[j]);
+    } else if (next < freed.size()) {
+      slot_out[j] = freed[next++];
+    } else {
+      slot_out[j] = grow++;
+    }
+  }
+  if (grow > new_n) return fail(PG_ERR_INVALID, "hof_update_packed: slots beyond the new hall (%d > %d)", grow, new_n);
+  return PG_OK;
+}
+}  // namespace
+
 int32_t pg_hof_update_packed(const pg_hof_packed_args *a) {
   if (!a) return fail(PG_ERR_INVALID, "args is NULL");
   const int hn = a->hof_n, k = a->k;
   if (a->maxsize < 0 || hn < 0 || hn > a->maxsize || k < 0 || !a->new_n || (a->maxsize > 0 && (!a->new_src || !a->new_fitness)) ||
       (hn > 0 && !a->hof_fitness) || (hn + k > 0 && !a->packed))
     return fail(PG_ERR_INVALID, "hof_update_packed: bad sizes or NULL buffers");
+  if (a->slot_in)
+    for (int e = 0; e < hn; ++e)
+      if (a->slot_in[e] < 0 || a->slot_in[e] >= hn)
+        return fail(PG_ERR_INVALID, "hof_update_packed: slot_in[%d]=%d outside [0, hof_n)", e, a->slot_in[e]);
   const int64_t *pk = a->packed;
   const int n = hn + k;
   auto rank_of = [&](int e) { return (int32_t)(uint32_t)pk[e]; };
@@ -1276,7 +1309,9 @@ int32_t pg_hof_update_packed(const pg_hof_packed_args *a) {
     g.new_n = a->new_n;
     g.new_src = a->new_src;
     g.new_fitness = a->new_fitness;
-    return pg_hof_update(&g);
+    const int32_t rc = pg_hof_update(&g);
+    if (rc != PG_OK || !a->slot_out) return rc;
+    return assign_slots(hn, *a->new_n, a->slot_in, a->new_src, a->slot_out);
   };
   if (a->maxsize == 0) {
     *a->new_n = 0;
@@ -1338,6 +1373,19 @@ int32_t pg_hof_update_packed(const pg_hof_packed_args *a) {
   // items order: members 0..p (descending rank) merged with the present
   // candidates by descending rank (the bitmap walked down), member runs
   // copied as ranges
+  // (slot_out: a member run keeps its slots; a candidate takes the next freed
+  // slot -- the evicted tail p+1..hn-1's, then hn, hn + 1, ...)
+  int32_t *so = a->slot_out;
+  int freed = p + 1, grow = hn;
+  const auto member_run = [&](int j0, int from, int to) {
+    for (int e = from; e < to; ++e) a->new_src[j0 + e - from] = e;
+    std::memcpy(a->new_fitness + j0, a->hof_fitness + from, sizeof(double) * (size_t)(to - from));
+    if (so) {
+      if (a->slot_in) std::memcpy(so + j0, a->slot_in + from, sizeof(int32_t) * (size_t)(to - from));
+      else
+        for (int e = from; e < to; ++e) so[j0 + e - from] = e;
+    }
+  };
   int j = 0, m = 0;  // output position, next member
   for (size_t wd = cbits.size(); wd-- > 0;) {
     uint64_t bits = cbits[wd];
@@ -1347,19 +1395,19 @@ int32_t pg_hof_update_packed(const pg_hof_packed_args *a) {
       const int r = (int)(wd * 64 + hi), c = cand_at[r];
       int lo = m;  // the members ranked above this candidate
       while (lo <= p && rank_of(lo) > r) ++lo;
-      for (int e = m; e < lo; ++e) a->new_src[j + e - m] = e;
-      std::memcpy(a->new_fitness + j, a->hof_fitness + m, sizeof(double) * (size_t)(lo - m));
+      member_run(j, m, lo);
       j += lo - m;
       m = lo;
       a->new_src[j] = hn + c;
       a->new_fitness[j] = cand_fit(c);
+      if (so) so[j] = freed < hn ? (a->slot_in ? a->slot_in[freed++] : freed++) : grow++;
       ++j;
     }
   }
-  for (int e = m; e <= p; ++e) a->new_src[j + e - m] = e;
-  if (p + 1 > m) std::memcpy(a->new_fitness + j, a->hof_fitness + m, sizeof(double) * (size_t)(p + 1 - m));
-  j += p + 1 - m;
+  if (p + 1 > m) member_run(j, m, p + 1);
+  j += p + 1 > m ? p + 1 - m : 0;
   *a->new_n = j;
+  if (so && grow > j) return fail(PG_ERR_INVALID, "hof_update_packed: slots beyond the new hall (%d > %d)", grow, j);
   return PG_OK;
 }
 

@@ -16,7 +16,7 @@ LIB_NAME = "libpong_ga.so"
 LIB_PATH = os.environ.get("PONG_GA_LIB") or os.path.join(PKG_DIR, LIB_NAME)  # override: variant builds
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pong_ga.h")
 
-PG_ABI_VERSION = 11
+PG_ABI_VERSION = 12
 PG_MAX_NODES = 9
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
@@ -119,7 +119,8 @@ class PgScheduleArgs(ctypes.Structure):
 
 class PgHofPackedArgs(ctypes.Structure):
     _fields_ = [("maxsize", ctypes.c_int32), ("hof_n", ctypes.c_int32), ("hof_fitness", _vp), ("k", ctypes.c_int32),
-                ("packed", _vp), ("new_n", _vp), ("new_src", _vp), ("new_fitness", _vp)]
+                ("packed", _vp), ("new_n", _vp), ("new_src", _vp), ("new_fitness", _vp),
+                ("slot_in", _vp), ("slot_out", _vp)]  # ABI 12: the hall in place
 
 
 class PgHofArgs(ctypes.Structure):
@@ -178,6 +179,7 @@ class PgHofCommitArgs(ctypes.Structure):
         ("rows", _vp), ("rows_stride", ctypes.c_int64), ("cand", _vp), ("src", _vp), ("n_old", ctypes.c_int32),
         ("m", ctypes.c_int32), ("genes", ctypes.c_int64), ("dtype", ctypes.c_int32), ("old_hash", _vp),
         ("cand_hash", _vp), ("new_hash", _vp), ("fitness_in", _vp), ("new_fitness", _vp),
+        ("dst_slot", _vp),  # ABI 12: the hall in place
     ]
 
 

@@ -610,23 +610,43 @@ def hof_update(maxsize: int, hof_fitness, hof_hash, pop_fitness, pop_hash, rank=
     return src[: new_n.value].copy(), fit[: new_n.value].copy()
 
 
-def hof_update_packed(maxsize: int, hof_fitness, packed, k: int):
+def hof_update_packed(maxsize: int, hof_fitness, packed, k: int, slot_in=None, slots: bool = False, out=None):
     """pg_hof_update_packed (host, no GPU): HallOfFame.update from the device's
     packing (pg_hof_prepare_cand: rank | class << 32 per member then per
     candidate, then the candidates' fitness bits); returns (src, fitness) as
-    hof_update does."""
+    hof_update does, and with ``slots`` the new members' storage slots too
+    (the hall in place, ABI 12: ``slot_in`` the current members' slots, None
+    = identity).  ``out``: optional int32 numpy array of >= 4 * maxsize
+    entries (e.g. a pinned buffer's view) that receives fitness (as f64 in its
+    first 2 * maxsize), src and slots back to back -- ready for one upload."""
     import numpy as np
     hf = np.ascontiguousarray(hof_fitness, dtype=np.float64)
     pk = np.ascontiguousarray(packed, dtype=np.int64)
     if pk.shape[0] < hf.shape[0] + 2 * k:
         raise ValueError("packed must hold hof_n + 2k entries")
-    src = np.empty(max(maxsize, 1), dtype=np.int32)
-    fit = np.empty(max(maxsize, 1), dtype=np.float64)
+    M = max(maxsize, 1)
+    if out is not None:
+        if out.dtype != np.int32 or out.ndim != 1 or out.shape[0] < 4 * M or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous int32 array of >= 4 * maxsize entries")
+        fit, src, slot = out[: 2 * M].view(np.float64), out[2 * M:3 * M], out[3 * M:4 * M]
+    else:
+        src = np.empty(M, dtype=np.int32)
+        fit = np.empty(M, dtype=np.float64)
+        slot = np.empty(M, dtype=np.int32)
+    sin = None
+    if slot_in is not None:
+        sin = np.ascontiguousarray(slot_in, dtype=np.int32)
+        if sin.shape[0] < hf.shape[0]:
+            raise ValueError("slot_in must hold hof_n entries")
     new_n = ctypes.c_int32(0)
     a = L.PgHofPackedArgs(maxsize, hf.shape[0], hf.ctypes.data, int(k), pk.ctypes.data, ctypes.addressof(new_n),
-                          src.ctypes.data, fit.ctypes.data)
+                          src.ctypes.data, fit.ctypes.data, sin.ctypes.data if sin is not None else None,
+                          slot.ctypes.data if slots else None)
     L.check("pg_hof_update_packed", L.lib().pg_hof_update_packed(ctypes.byref(a)))
-    return src[: new_n.value], fit[: new_n.value]
+    n = new_n.value
+    if slots:
+        return src[:n], fit[:n], slot[:n]
+    return src[:n], fit[:n]
 
 
 FRAME_SHAPE = (210, 160, 3)  # obs.npy
@@ -789,21 +809,34 @@ def hof_prepare_cand(hof_fitness: torch.Tensor, hof_hash: torch.Tensor, cand: to
         L.check("pg_hof_prepare_cand", L.lib().pg_hof_prepare_cand(ctypes.byref(a), _stream(dev)))
 
 
-def hof_commit(dst: torch.Tensor, old_rows: torch.Tensor, rows: torch.Tensor, cand: torch.Tensor, src: torch.Tensor,
-               n_old: int, genes: int, old_hash: torch.Tensor, cand_hash: torch.Tensor, new_hash: torch.Tensor,
-               fitness_in: torch.Tensor, new_fitness: torch.Tensor) -> None:
-    """pg_hof_commit: the new members' rows, hashes and fitness in one pass."""
+def hof_commit(dst: torch.Tensor, old_rows: Optional[torch.Tensor], rows: torch.Tensor, cand: torch.Tensor,
+               src: torch.Tensor, n_old: int, genes: int, old_hash: torch.Tensor, cand_hash: torch.Tensor,
+               new_hash: torch.Tensor, fitness_in: torch.Tensor, new_fitness: torch.Tensor,
+               dst_slot: Optional[torch.Tensor] = None) -> None:
+    """pg_hof_commit: the new members' rows, hashes and fitness in one pass;
+    with ``dst_slot`` (ABI 12) the hall in place: ``dst`` is the hall's
+    storage, member j's row is dst[dst_slot[j]], and only entering
+    candidates' rows are written (``old_rows`` unused, may be None)."""
     dev = dst.device
     m = src.shape[0]
     _need(src, "src", torch.int32, dev, (m,))
     _need(fitness_in, "fitness_in", torch.float64, dev, (m,))
+    if dst_slot is not None:
+        _need(dst_slot, "dst_slot", torch.int32, dev, (m,))
+        old_rows = None
+    elif old_rows is None:
+        raise ValueError("old_rows is required without dst_slot")
     for name, t in (("dst", dst), ("old_rows", old_rows), ("rows", rows)):
+        if t is None:
+            continue
         if t.dim() != 2 or t.dtype != dst.dtype or t.device != dev or t.stride(1) != 1:
             raise ValueError(f"{name} must be a row-major [n, G] tensor of dst's dtype on dst's device")
     if m > dst.shape[0] or m > new_hash.shape[0] or m > new_fitness.shape[0]:
         raise ValueError("more members than destination rows")
-    a = L.PgHofCommitArgs(_ptr(dst), dst.stride(0), _ptr(old_rows), old_rows.stride(0), _ptr(rows), rows.stride(0),
+    a = L.PgHofCommitArgs(_ptr(dst), dst.stride(0), _ptr(old_rows) if old_rows is not None else None,
+                          old_rows.stride(0) if old_rows is not None else 0, _ptr(rows), rows.stride(0),
                           _ptr(cand), _ptr(src), int(n_old), m, int(genes), DTYPES[dst.dtype], _ptr(old_hash),
-                          _ptr(cand_hash), _ptr(new_hash), _ptr(fitness_in), _ptr(new_fitness))
+                          _ptr(cand_hash), _ptr(new_hash), _ptr(fitness_in), _ptr(new_fitness),
+                          _ptr(dst_slot) if dst_slot is not None else None)
     with torch.cuda.device(dev):
         L.check("pg_hof_commit", L.lib().pg_hof_commit(ctypes.byref(a), _stream(dev)))

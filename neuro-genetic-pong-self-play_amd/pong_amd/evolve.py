@@ -15,7 +15,14 @@ Generation 0 evaluates the initial population and fills the hall of fame.
 
 Storage: one ``[H + P, G]`` buffer, hall-of-fame rows first, and a spare of
 the same shape that the next generation is written into, so neither the
-variation nor the hall-of-fame gather reads what it writes.  The GA state is
+variation nor the hall-of-fame gather reads what it writes.  The fused path
+keeps the hall IN PLACE (``in_place_hall``, ABI 12): its rows stay in the
+first buffer's H rows, member j (items order) in slot ``hof_slot[j]``; an
+update writes only the entering candidates' rows, into the slots of the
+members they evict (pg_hof_update_packed's slot_out, pg_hof_commit's
+dst_slot), where the dense form rewrote all H rows into the spare buffer.
+Games index hall positions (the schedule); the evaluation maps them to slots
+(or, with a sliced hall, gathers the rank's slice, H/N rows).  The GA state is
 replicated on every rank; rank r evaluates rows ``shard_range(P, r, N)`` and
 the fitness vector is all-gathered once per generation -- the only collective.
 
@@ -98,6 +105,14 @@ class DeviceGA:
                        if self.hof_slices > 1 and self.hi > self.lo and self.lo // B == (self.hi - 1) // B else None)
         self.store = torch.zeros((self.H + self.P, self.G), dtype=dtype, device=self.device)
         self.spare = torch.empty_like(self.store)
+        # the hall in place (fused path): the first buffer's hall rows, fixed
+        # across the store/spare swaps; member j's row is _hall_buf[hof_slot[j]]
+        self.in_place_hall = True
+        self._hall_buf = self.store[: self.H]
+        self.hof_slot = torch.arange(max(self.H, 1), dtype=torch.int32, device=self.device)
+        self._hof_slot_h = np.zeros(0, np.int32)
+        self._slots_identity = True
+        self._up_keep = None
         self.fitness = torch.zeros(self.P, dtype=torch.float64, device=self.device)
         self.valid = torch.zeros(self.P, dtype=torch.bool, device=self.device)
         self.hof_fitness = torch.zeros(max(self.H, 1), dtype=torch.float64, device=self.device)
@@ -166,10 +181,37 @@ class DeviceGA:
         return self._slice is not None and n_hof >= self.hof_slices
 
     def _opponents(self, buf: torch.Tensor, n_hof: int) -> Optional[torch.Tensor]:
-        """The hall rows this rank's games index: the whole hall, or its slice."""
+        """The hall rows this rank's games index: the whole hall, or its slice
+        (in place: the slots [0, n_hof) -- the schedule's positions go through
+        _opp_slots -- or the slice's rows gathered in position order)."""
         if not n_hof:
             return None
+        if self._in_place():
+            if self._sliced(n_hof):
+                idx = self.hof_slot[self._slice:n_hof:self.hof_slices].long()
+                out = self._buf("hall_slice", (idx.shape[0], self.G), self.dtype)
+                torch.index_select(self._hall_buf, 0, idx, out=out)
+                return out
+            return self._hall_buf[:n_hof]
         return buf[self._slice:n_hof:self.hof_slices] if self._sliced(n_hof) else buf[:n_hof]
+
+    def _in_place(self) -> bool:
+        return bool(self.in_place_hall and self.fused and self.H > 0)
+
+    def _opp_slots(self, opp: torch.Tensor, n_hof: int) -> torch.Tensor:
+        """The schedule's hall positions as the in-place hall's slots (a sliced
+        hall's local indices need nothing: its rows were gathered in order)."""
+        if not self._in_place() or not n_hof or self._sliced(n_hof) or self._slots_identity:
+            return opp
+        return torch.index_select(self.hof_slot[:n_hof], 0, opp.reshape(-1)).view_as(opp)
+
+    def _opponents_by_position(self, n_hof: int) -> Optional[torch.Tensor]:
+        """The opponents in the schedule's index order (for on_evaluate)."""
+        if not n_hof:
+            return None
+        if self._in_place() and not self._sliced(n_hof):
+            return self.hall_of_fame[:n_hof]
+        return self._opponents(self.store, n_hof)
 
     def eval_schedule(self, g: int, n_hof: Optional[int] = None, rows="last"):
         """(kind, opp, mult) of generation g's games for this rank's shard,
@@ -239,7 +281,10 @@ class DeviceGA:
 
     @property
     def hall_of_fame(self) -> torch.Tensor:
-        """Members, best first (HallOfFame.items order)."""
+        """Members, best first (HallOfFame.items order); the in-place hall's
+        rows gathered in that order (a copy)."""
+        if self._in_place():
+            return self._hall_buf[self.hof_slot[: self.hof_n].long()]
         return self.store[: self.hof_n]
 
     @property
@@ -300,6 +345,13 @@ class DeviceGA:
         self._next = None
         self.hof_n = n
         self._hof_fit_host = fit.copy()
+        # the in-place hall: slots = positions again, its rows from store[:n]
+        if n and self._hall_buf.data_ptr() != self.store.data_ptr():
+            self._hall_buf[:n] = self.store[:n]
+        if self.H:
+            self.hof_slot.copy_(torch.arange(self.hof_slot.shape[0], dtype=torch.int32, device=self.device))
+        self._hof_slot_h = np.arange(n, dtype=np.int32)
+        self._slots_identity = True
         if n:
             self.hof_fitness[:n] = torch.from_numpy(fit).to(self.device)
             self.hof_hash[:n] = D.row_hash(self.store[:n], self.G)
@@ -307,6 +359,8 @@ class DeviceGA:
     def _set_hof_empty(self):
         self.hof_n = 0
         self._hof_fit_host = np.zeros(0, np.float64)
+        self._hof_slot_h = np.zeros(0, np.int32)
+        self._slots_identity = True
 
     # ------------------------------------------------------------ steps
     def _evaluate(self, g: int, rows: torch.Tensor, inv: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -637,7 +691,12 @@ class DeviceGA:
         sched = self.eval_schedule(g, n_hof=self.H, rows=local)
         # the records land in the evaluator's workspace; the later PG_PREP_REST call
         # (same genomes, rows, count; opponents of the same size) adds the opponents'
-        self.ev.evaluate(off, *sched, opponents=self._opponents(self.spare, self.H), out=self.last, validate=False,
+        # (the opponents' rows are not read by a "genomes" preparation: the
+        # current hall stands in for the updated one, which has the same size)
+        opponents = self._hall_buf[: self.H] if self._in_place() else self._opponents(self.spare, self.H)
+        if self._in_place() and self._sliced(self.H):
+            opponents = self._hall_buf[self._slice:self.H:self.hof_slices]
+        self.ev.evaluate(off, *sched, opponents=opponents, out=self.last, validate=False,
                          hard_log=self.hard_log, rows=local, n_active=count, prep="genomes")
         return sched
 
@@ -659,6 +718,7 @@ class DeviceGA:
         else:  # made during the hall-of-fame scan with the genomes' records (_early_prep)
             kind, opp, mult = sched
         opponents = self._opponents(self.store, self.hof_n)
+        opp = self._opp_slots(opp, self.hof_n)
         out = self.last if (self.last is not None and self.last.fitness.shape[0] == n) else None
         if self.eval_events is not None:
             self.eval_events[0].record()
@@ -669,7 +729,7 @@ class DeviceGA:
             self.eval_events[1].record()
         self.last, self.last_rows, self.last_count = res, local, count
         if self.on_evaluate is not None:
-            self.on_evaluate(g, rows, opponents, res)
+            self.on_evaluate(g, rows, self._opponents_by_position(self.hof_n), res)
         if self._balanced():
             return self._gather_dealt(res, local, count)
         shard = self._buf("shard_fit", n, torch.float64)
@@ -712,8 +772,10 @@ class DeviceGA:
                 overlap()
             return
         old_n = self.hof_n
+        in_place = self._in_place()
         if k == 0:
-            dst[:old_n] = self.store[:old_n]
+            if not in_place:
+                dst[:old_n] = self.store[:old_n]
             if overlap:
                 overlap()
             return
@@ -751,21 +813,32 @@ class DeviceGA:
             self._mark("next_select_vary", sub=True)
         copied.synchronize()
         # the scan straight on the device's packing, visiting only the hall's
-        # tail and the candidates (pg_hof_update_packed, O(k log k))
-        src, new_fit = D.hof_update_packed(self.H, self._hof_fit_host, packed_h.numpy(), k)
+        # tail and the candidates (pg_hof_update_packed, O(k log k)); its
+        # outputs land in the pinned upload buffer: fitness, sources, slots
+        M = max(self.H, 1)
+        up = torch.empty(4 * M, dtype=torch.int32, pin_memory=True)
+        res = D.hof_update_packed(self.H, self._hof_fit_host, packed_h.numpy(), k, out=up.numpy(),
+                                  slot_in=self._hof_slot_h if in_place else None, slots=in_place)
+        src, new_fit = res[0], res[1]
         self._mark("hof_scan", sub=True)
         m = src.shape[0]
-        up = torch.empty(3 * m, dtype=torch.int32, pin_memory=True)
-        upn = up.numpy()
-        upn[: 2 * m].view(np.float64)[:] = new_fit
-        upn[2 * m:] = src
         up_d = up.to(self.device, non_blocking=True)
-        D.hof_commit(dst, self.store, rows, cand, up_d[2 * m:], old_n, self.G, self.hof_hash, cand_hash,
-                     self._hof_hash_alt, up_d[: 2 * m].view(torch.float64), self._hof_fitness_alt)
+        src_d, fit_d = up_d[2 * M:2 * M + m], up_d[: 2 * M].view(torch.float64)[:m]
+        if in_place:
+            slot_d = up_d[3 * M:3 * M + m]
+            D.hof_commit(self._hall_buf, None, rows, cand, src_d, old_n, self.G, self.hof_hash, cand_hash,
+                         self._hof_hash_alt, fit_d, self._hof_fitness_alt, dst_slot=slot_d)
+            self.hof_slot[:m].copy_(slot_d)
+            self._hof_slot_h = res[2]
+            self._slots_identity = False
+        else:
+            D.hof_commit(dst, self.store, rows, cand, src_d, old_n, self.G, self.hof_hash, cand_hash,
+                         self._hof_hash_alt, fit_d, self._hof_fitness_alt)
         self.hof_hash, self._hof_hash_alt = self._hof_hash_alt, self.hof_hash
         self.hof_fitness, self._hof_fitness_alt = self._hof_fitness_alt, self.hof_fitness
         self.hof_n = int(m)
         self._hof_fit_host = new_fit
+        self._up_keep = up  # _hof_fit_host (and _hof_slot_h) are views of it
         if side is not None:
             main.wait_stream(side)
 
@@ -791,7 +864,8 @@ class DeviceGA:
             # update); the initial population is current on every rank
             self._hof_update_fused(self._rows, cand, cand_fit, k, self.spare,
                                    overlap=lambda: self._next_gen_prep(1, self._rows, new_fit, self.spare))
-            self.store[: self.hof_n] = self.spare[: self.hof_n]
+            if not self._in_place():
+                self.store[: self.hof_n] = self.spare[: self.hof_n]
             self.generation = 0
             return self._record(0, nevals, stats)
         g = self.generation + 1

@@ -250,3 +250,35 @@ def test_vary_pair_list_equals_mask(gpu, dtype):
         w[2 * j: min(2 * j + 2, P)] = True
     assert torch.equal(out[w], full[w]) and bool((out[~w] == 7.0).all())
     assert torch.equal(inv[w], inv_full[w]) and bool((inv[~w] == 9).all())
+
+
+@pytest.mark.parametrize("schedule,dtype,P,H,slices", [("selfplay", torch.float64, 2048, 512, 0),
+                                                       ("reference", torch.float32, 600, 150, 0),
+                                                       ("selfplay", torch.float64, 4096, 1024, 1024)])
+def test_in_place_hall_equals_dense_commit(gpu, schedule, dtype, P, H, slices):
+    """The hall kept in place (ABI 12: pg_hof_update_packed's slots,
+    pg_hof_commit's dst_slot, the schedule's positions mapped to slots or a
+    sliced hall's rows gathered) against the dense commit that rewrites the
+    whole hall every generation: the same populations, fitness, halls, hashes
+    and logbooks generation by generation."""
+    from pong_amd.evolve import DeviceGA
+    runs = []
+    for in_place in (True, False):
+        ga = DeviceGA([6, 16, 3], P, hof_size=H, tournsize=max(P // 4, 1), dtype=dtype, device=gpu,
+                      schedule=schedule, seed=31, hof_block_rows=slices)
+        ga.in_place_hall = in_place
+        ga.initialize("normal", 3.0)
+        halls = []
+        for _ in range(6):
+            ga.step()
+            halls.append((ga.hall_of_fame.clone(), ga.hof_hash[: ga.hof_n].clone()))
+        runs.append((ga, halls))
+    (a, ha), (b, hb) = runs
+    assert not a._slots_identity  # the slots did move
+    for (ra, sa), (rb, sb) in zip(ha, hb):
+        assert torch.equal(ra, rb) and torch.equal(sa, sb)
+    assert torch.equal(a.population, b.population) and torch.equal(a.fitness, b.fitness)
+    assert a.hof_member_fitness.tolist() == b.hof_member_fitness.tolist()
+    assert a.logbook == b.logbook
+    # the in-place hall's storage holds each member in its slot
+    assert torch.equal(a._hall_buf[a.hof_slot[: a.hof_n].long()], b.hall_of_fame)

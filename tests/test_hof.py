@@ -211,3 +211,76 @@ def test_hof_update_packed_unordered_members_fall_back():
     src_g, fit_g = D.hof_update(H, mf, cls[:H], pf, cls[H:], rank=(packed[:H + 50] & 0xFFFFFFFF).astype(np.int32))
     np.testing.assert_array_equal(src_p, src_g)
     np.testing.assert_array_equal(fit_p, fit_g)
+
+
+def _check_slots(old_slots, old_ids, src, slots, old_n):
+    """The in-place hall's invariants: a storage array of ids (slot -> entry)
+    updated by writing only the entering candidates holds member j's id in
+    slot[j]; kept members kept their slots; the slots in use are [0, new_n)."""
+    m = src.shape[0]
+    store = np.full(max(m, old_n, 1), -1, np.int64)
+    store[old_slots[:old_n]] = old_ids[:old_n]
+    for j in range(m):
+        if src[j] >= old_n:
+            store[slots[j]] = 10**9 + src[j]  # a candidate's id
+        else:
+            assert slots[j] == old_slots[src[j]]  # a kept member stays in place
+    ids = np.array([old_ids[s] if s < old_n else 10**9 + s for s in src], np.int64)
+    np.testing.assert_array_equal(store[slots], ids)
+    assert sorted(slots.tolist()) == list(range(m))
+    return ids
+
+
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("unordered", [False, True])
+def test_hof_update_packed_slots(seed, unordered):
+    """pg_hof_update_packed's slot_out (ABI 12, the hall kept in place) over
+    successive updates, on the packed scan and on its general fallback
+    (unordered members): the same members as without slots, and a storage
+    that receives only the entering candidates' rows holds every member in
+    its slot."""
+    rng = np.random.default_rng(7000 + seed)
+    maxsize = int(rng.integers(1, 200))
+    keys_f, keys_h = np.zeros(0), np.zeros(0, np.int64)
+    slots, ids = np.zeros(0, np.int32), np.zeros(0, np.int64)
+    genes = rng.integers(-2**62, 2**62, size=int(rng.integers(2, 300)))
+    for gen in range(6):
+        n = int(rng.integers(0, 400))
+        fit = np.round(rng.standard_normal(n) * 2, int(rng.integers(0, 3)))
+        hsh = genes[rng.integers(0, genes.size, size=n)]
+        mf = keys_f
+        if unordered and mf.shape[0] > 1:  # members out of items order: the general scan
+            perm = rng.permutation(mf.shape[0])
+            mf, keys_h, slots, ids = mf[perm], keys_h[perm], slots[perm], ids[perm]
+        packed = _packing(mf, keys_h, fit, hsh)
+        src0, fit0 = D.hof_update_packed(maxsize, mf, packed, n)
+        src, new_fit, new_slots = D.hof_update_packed(maxsize, mf, packed, n, slot_in=slots, slots=True)
+        np.testing.assert_array_equal(src, src0)
+        np.testing.assert_array_equal(new_fit, fit0)
+        old_n = mf.shape[0]
+        ids = _check_slots(slots, ids, src, new_slots, old_n) + gen * 10**10 * (src >= old_n)
+        keys_h = np.array([keys_h[s] if s < old_n else hsh[s - old_n] for s in src], dtype=np.int64)
+        keys_f, slots = new_fit.copy(), new_slots.copy()
+
+
+def test_hof_update_packed_slots_large_out_buffer():
+    """Config 4's sizes with the outputs written into one upload buffer
+    (fitness, sources, slots back to back), as DeviceGA passes it."""
+    rng = np.random.default_rng(11)
+    H, k = 131072, 18721
+    hof_f = np.sort(rng.normal(size=H))[::-1].copy()
+    hof_h = rng.integers(-2**62, 2**62, size=H)
+    fit = rng.normal(size=k) + 2.0
+    hsh = rng.integers(-2**62, 2**62, size=k)
+    slots = rng.permutation(H).astype(np.int32)
+    packed = _packing(hof_f, hof_h, fit, hsh)
+    out = np.zeros(4 * H, np.int32)
+    src, new_fit, new_slots = D.hof_update_packed(H, hof_f, packed, k, slot_in=slots, slots=True, out=out)
+    src0, fit0 = D.hof_update_packed(H, hof_f, packed, k)
+    np.testing.assert_array_equal(src, src0)
+    np.testing.assert_array_equal(new_fit, fit0)
+    np.testing.assert_array_equal(out[2 * H:2 * H + src.shape[0]], src)
+    np.testing.assert_array_equal(out[:2 * H].view(np.float64)[:src.shape[0]], fit0)
+    _check_slots(slots, np.arange(H, dtype=np.int64), src, new_slots, H)
+    with pytest.raises(ValueError):
+        D.hof_update_packed(H, hof_f, packed, k, out=np.zeros(4 * H - 1, np.int32))

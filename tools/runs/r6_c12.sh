@@ -14,3 +14,6 @@ done
 timeout -k 10 900 python3 -u bench.py --config wide --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_wide.json 2>> $OUT/err.log || exit 1
 timeout -k 10 900 python3 -u tools/scale_model_wide.py 2 > $OUT/scale_model_wide.log 2>&1 || exit 1
 echo done > $OUT/ok
+# the replicated GA work at P = 8 x 65 536 with the packed hall-of-fame scan
+timeout -k 10 600 python3 -u tools/scale_model.py 8 4 > $OUT/scale_model.log 2>&1 || exit 1
+echo done2 > $OUT/ok2

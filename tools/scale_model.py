@@ -76,12 +76,13 @@ def shard_evals(ga, n_shards):
     P, S = ga.P, ga.P // n_shards
     ev = D.Evaluator(ga.nodes, dtype=ga.dtype, device=ga.device, n_games=ga.n_games, seed=ga.ev.seed)
     K = ga.hof_slices
+    hof = ga.hall_of_fame  # (items order; the in-place hall's rows gathered once)
     ms = []
     for r in range(n_shards):
         lo = r * S
         # what rank r plays: its block's slice of the hall (bench.py's schedule)
         sliced = K > 1 and ga.hof_n >= K and S == ga.hof_block_rows
-        opponents = ga.hall_of_fame[r % K::K] if sliced else ga.hall_of_fame[: ga.hof_n]
+        opponents = hof[r % K::K] if sliced else hof[: ga.hof_n]
         kind, opp, mult = D.schedule("selfplay", S, ga.n_games, lo, ga.hof_fitness, ga.hof_n, ga.seed,
                                      ga.generation + 1, ga.device, hof_slices=K, block_rows=ga.hof_block_rows,
                                      slice_local=sliced)
@@ -179,27 +180,58 @@ def replicated_ops(ga, n_shards=1, reps=3):
                                                        cand_fit[:k], ga._rows, ga.G, ch, pk, ga.ws))
         pk_h = pk.cpu().numpy()
         n = old_n + k
+        # the scan DeviceGA runs (pg_hof_update_packed straight on the device's
+        # packing, with the in-place hall's slots), and beside it the general
+        # scan it replaced (pg_hof_update)
+        in_place = ga._in_place()
         t0 = time.perf_counter()
-        src, nf = D.hof_update(ga.H, ga._hof_fit_host, (pk_h[:old_n] >> 32), pk_h[n:].view(np.float64),
-                               pk_h[old_n:n] >> 32, rank=(pk_h[:n] & 0xFFFFFFFF).astype(np.int32))
+        r = D.hof_update_packed(ga.H, ga._hof_fit_host, pk_h, k, slot_in=ga._hof_slot_h if in_place else None,
+                                slots=in_place)
         out["hof_scan_host"] = (time.perf_counter() - t0) * 1e3
+        src, nf = r[0], r[1]
+        t0 = time.perf_counter()
+        D.hof_update(ga.H, ga._hof_fit_host, (pk_h[:old_n] >> 32), pk_h[n:].view(np.float64),
+                     pk_h[old_n:n] >> 32, rank=(pk_h[:n] & 0xFFFFFFFF).astype(np.int32))
+        out["hof_scan_host_general"] = (time.perf_counter() - t0) * 1e3
         m = src.shape[0]
+        out["hof_entering"] = int((src >= old_n).sum())
         src_d = torch.tensor(src, dtype=torch.int32, device=dev)
         nf_d = torch.tensor(nf, dtype=torch.float64, device=dev)
         hh = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
         hf = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
+        if in_place:  # into a copy of the hall: the GA's own state stays as it is
+            hall = ga._hall_buf.clone()
+            slot_d = torch.tensor(r[2], dtype=torch.int32, device=dev)
+            timed("hof_commit", lambda: D.hof_commit(hall, None, ga._rows, cand[:k], src_d, old_n, ga.G,
+                                                     ga.hof_hash, ch, hh, nf_d, hf, dst_slot=slot_d))
+            del hall
         dst = torch.empty((m, ga.G), dtype=ga.dtype, device=dev)
-        timed("hof_commit", lambda: D.hof_commit(dst, ga.store, ga._rows, cand[:k], src_d, old_n, ga.G,
-                                                 ga.hof_hash, ch, hh, nf_d, hf))
+        timed("hof_commit_dense" if in_place else "hof_commit",
+              lambda: D.hof_commit(dst, ga.store, ga._rows, cand[:k], src_d, old_n, ga.G,
+                                   ga.hof_hash, ch, hh, nf_d, hf))
+        del dst
+        if in_place and n_shards > 1:
+            # a rank's slice of the in-place hall (its block plays hall[b::N]):
+            # gathered in position order before its evaluation
+            idx = ga.hof_slot[0:ga.hof_n:n_shards].long()
+            sl = torch.empty((idx.shape[0], ga.G), dtype=ga.dtype, device=dev)
+            timed("hall_slice_gather", lambda: torch.index_select(ga._hall_buf, 0, idx, out=sl))
+            del sl
     # on the critical path: merge, the candidates' completion (sharded), their
     # prepare and commit; the selection, the parents' completion, the shard's
     # variation and inheritance run on the side stream beside the host scan
     # (evolve.py)
     dev_serial = (out.get("merge", 0) + out.get("complete_cand", 0) + out.get("hof_prepare", 0)
-                  + out.get("hof_commit", 0))
+                  + out.get("hof_commit", 0) + out.get("hall_slice_gather", 0))
     side = out["select_ranked"] + out.get("complete_parents", 0) + out["vary"] + out["inherit"]
     overlapped = max(side, out.get("hof_scan_host", 0.0))
     out["replicated_critical_ms"] = dev_serial + overlapped
+    # the code's stream structure (evolve._hof_update_fused): the side stream
+    # starts right after the candidates' completion and runs beside the
+    # prepare, the host scan and the commit; the slice gather follows both
+    main = out.get("hof_prepare", 0) + out.get("hof_scan_host", 0) + out.get("hof_commit", 0)
+    out["replicated_critical_ms_streams"] = (out.get("merge", 0) + out.get("complete_cand", 0)
+                                             + out.get("hall_slice_gather", 0) + max(side, main))
     return out
 
 
@@ -246,17 +278,67 @@ def main():
     ops = replicated_ops(gaN, N)
     print(json.dumps({"replicated_ops_pN": ops}), flush=True)
     res["replicated_ops_pN"] = ops
+    # Why the one-GPU run at P has a longer non-evaluation wall than the model's
+    # rank: it prepares the lane records of all P genomes (during the hall-of-
+    # fame scan, outside the evaluation's events) where a rank prepares its
+    # shard's, and its per-row order / scatter passes run over P rows.  The
+    # P-row genome preparation, timed against a shard's:
+    ev = D.Evaluator(gaN.nodes, dtype=gaN.dtype, device=dev, n_games=gaN.n_games, seed=gaN.ev.seed)
+    kind, opp, mult = D.schedule("selfplay", gaN.P, gaN.n_games, 0, gaN.hof_fitness, gaN.hof_n, gaN.seed,
+                                 gaN.generation + 1, dev)
+    prep = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ev.evaluate(gaN._rows, kind, opp, mult, opponents=gaN.hall_of_fame[:gaN.hof_n], validate=False,
+                    prep="genomes")
+        b.record()
+        torch.cuda.synchronize()
+        prep.append(a.elapsed_time(b))
+    res["genome_prep_ms_all_P"] = float(np.median(prep))
+    res["genome_prep_ms_shard"] = float(np.median([s[0][2] for s in shards]))
+    del ev
+    # the other per-row side-stream work of the one-GPU run at P that a rank
+    # does for its shard only: the evaluation order and the schedule
+    def dev_ms(fn, reps=3):
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return float(np.median(ts))
+    inv = torch.ones(gaN.P, dtype=torch.uint8, device=dev)
+    lr = torch.empty(gaN.P, dtype=torch.int32, device=dev)
+    lc = torch.empty(1, dtype=torch.int32, device=dev)
+    res["order_ms_all_P"] = dev_ms(lambda: D.order(gaN.P, 0, inv, gaN.lineage_frames, True, lr, lc, gaN.ws))
+    res["order_ms_shard"] = dev_ms(lambda: D.order(S, 0, inv, gaN.lineage_frames, True, lr[:S], lc, gaN.ws))
+    res["schedule_ms_all_P"] = dev_ms(lambda: D.schedule("selfplay", gaN.P, gaN.n_games, 0, gaN.hof_fitness,
+                                                        gaN.hof_n, gaN.seed, gaN.generation + 1, dev))
+    res["schedule_ms_shard"] = dev_ms(lambda: D.schedule("selfplay", S, gaN.n_games, 0, gaN.hof_fitness,
+                                                        gaN.hof_n, gaN.seed, gaN.generation + 1, dev))
     repl1 = float(np.median([w - e for w, e, _ in t1]))
     # a rank at N pays the one-GPU generation's non-evaluation time plus what
     # its P = N x 65 536 ops (sharded variation) cost beyond the same ops at
     # 65 536; its shard-sized work (evaluation prep, order, scatter) as at N = 1
     replN = repl1 + max(0.0, ops["replicated_critical_ms"] - ops1["replicated_critical_ms"])
     res["replicated_ms_pN_wall"] = float(np.median([w - e for w, e in zip(walls, evals)]))
+    # the one-GPU wall at P less the P-row record preparation a rank does not
+    # pay (it prepares its shard's rows, as at N = 1): against replicated_ms_pN
+    res["replicated_ms_pN_wall_less_prep"] = (res["replicated_ms_pN_wall"] - res["genome_prep_ms_all_P"]
+                                              + res["genome_prep_ms_shard"])
+    res["replicated_ms_pN_wall_less_row_work"] = (res["replicated_ms_pN_wall_less_prep"]
+                                                  - res["order_ms_all_P"] + res["order_ms_shard"]
+                                                  - res["schedule_ms_all_P"] + res["schedule_ms_shard"])
     shard_max = float(np.median([max(x[0] for x in s) for s in shards]))
     shard_mean = float(np.median([float(np.mean([x[0] for x in s])) for s in shards]))
     steps_n = float(np.median([sum(x[1] for x in s) for s in shards]))  # all ranks' stepped env-steps
     allgather = 0.03 + N * S * 12 / 1e12 * 1e3  # ms
     t_n = shard_max + replN + allgather
+    replN_s = repl1 + max(0.0, ops["replicated_critical_ms_streams"] - ops1["replicated_critical_ms_streams"])
+    t_n_s = shard_max + replN_s + allgather
     t_1 = float(np.median(res["p65536_wall_ms"]))  # the measured one-GPU generation
     steps_1 = float(np.median(res["p65536_steps"]))
     ps_1 = float(np.median(res["p65536_ps_per_step"]))
@@ -268,6 +350,9 @@ def main():
                 "ps_per_step_shard_pN": ps_n, "ps_per_step_one_gpu": ps_1,
                 "allgather_ms_model": allgather, "t1_ms": t_1, "tN_ms": t_n, "projected_efficiency": t_1 / t_n,
                 "projected_speedup": N * t_1 / t_n,
+                # the same with the critical path of the code's stream structure
+                "replicated_ms_pN_streams": replN_s, "tN_ms_streams": t_n_s,
+                "projected_efficiency_streams": t_1 / t_n_s,
                 "projected_env_steps_per_s_N": steps_n / (t_n / 1e3),
                 "env_steps_per_s_1": steps_1 / (t_1 / 1e3),
                 "projected_efficiency_env_steps": (steps_n / t_n) / (N * steps_1 / t_1)})

@@ -26,16 +26,16 @@ from pong_amd import dist as PD  # noqa: E402
 from pong_amd.evolve import DeviceGA  # noqa: E402
 
 
-def timed_eval(ga, rows_idx):
+def timed_eval(ga, rows_idx, hof):
     """One evaluation of the given population rows (in that order) against the
-    hall: (ms by HIP events, stepped env-steps)."""
+    hall (``hof``: its rows in items order): (ms by HIP events, stepped env-steps)."""
     dev = ga.device
     rows = torch.as_tensor(rows_idx, dtype=torch.int32, device=dev)
     kind, opp, mult = ga.eval_schedule(ga.generation + 1, rows=rows)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     a.record()
-    res, _ = ga.ev.evaluate(ga._rows, kind, opp, mult, opponents=ga.store[:ga.hof_n], validate=False, rows=rows)
+    res, _ = ga.ev.evaluate(ga._rows, kind, opp, mult, opponents=hof, validate=False, rows=rows)
     b.record()
     torch.cuda.synchronize()
     return a.elapsed_time(b), int(res.counters[0].item())
@@ -55,7 +55,8 @@ def main(gens=2, P=65536):
     lineage = ga.lineage_frames.cpu().numpy()
     # the whole population in one evaluation, longest lineage first (what one GPU plays)
     order = np.argsort(-lineage, kind="stable")
-    one_ms, one_steps = timed_eval(ga, order)
+    hof = ga.hall_of_fame
+    one_ms, one_steps = timed_eval(ga, order, hof)
     out = {"P": P, "generations": gens, "one_gpu_ms": one_ms, "one_gpu_steps": one_steps}
     print(json.dumps(out), flush=True)
     for N in (2, 4, 8):
@@ -69,7 +70,7 @@ def main(gens=2, P=65536):
                 else:
                     pos = PD.deal_positions(-(-P // N), r, N).numpy()
                     idx = order[pos[pos < P]]
-                m, s = timed_eval(ga, idx)
+                m, s = timed_eval(ga, idx, hof)
                 ms.append(m)
                 steps.append(s)
             rec = {"N": N, "mode": mode, "shard_ms": ms, "shard_steps": steps, "max_ms": max(ms),
