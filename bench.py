@@ -423,8 +423,29 @@ def wide_report(args, world, shape, G, dtype, P, n_local, H, tournsize, elapsed,
                      "survey_algorithmic_GBps": survey_bytes / (kernel_ms_mean / 1e3) / 1e9,
                      "note": "achieved = genome bytes streamed (network passes x genes x 4 B) / launch time; "
                              "survey_algorithmic counts both networks' genes per env-step (SURVEY 8d), which the "
-                             "lockstep genome pass amortises over the genome's games"},
+                             "lockstep genome pass amortises over the genome's games",
+                     **_measured_ceiling(achieved)},
     }
+
+
+def _measured_ceiling(achieved_gbps):
+    """The box's measured streaming-read ceiling beside the spec: the best rate
+    of tools/hbm_ceiling.hip (k_wide's load shape -- 1-KB line-aligned
+    non-temporal wave pieces, 512-thread blocks -- over an 8-16 GiB buffer read
+    once per pass, far past the 256 MiB Infinity Cache) in
+    profiles/<round>/hbm_ceiling.jsonl, when that run is on file."""
+    path = os.path.join(REPO, "profiles", PROFILE_ROUND, "hbm_ceiling.jsonl")
+    try:
+        runs = [json.loads(line) for line in open(path) if line.strip()]
+    except OSError:
+        return {"measured_ceiling_GBps": None}
+    best = max(runs, key=lambda r: r["best_TBps"])
+    ceil = best["best_TBps"] * 1e3
+    return {"measured_ceiling_GBps": ceil, "frac_of_measured_ceiling": achieved_gbps / ceil,
+            "measured_ceiling_source": "profiles/%s/hbm_ceiling.jsonl: best of %d configurations (%d blocks of 512, "
+                                       "%d pieces in flight per wave, %.0f GiB)"
+                                       % (PROFILE_ROUND, len(runs), best["grid"], best["pieces_in_flight_per_wave"],
+                                          best["bytes"] / 2**30)}
 
 
 def cpu_baseline(args, shape, ga, chunk=256, max_rows=1 << 16, pool=None):
