@@ -115,7 +115,7 @@ __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, In
   // frame bound does not follow (PG_INLINE_FRAME_BOUND=0): under the frame's
   // bound the same rule decides everything it would (round 6: it settled
   // 0.1 % of the bench's requests and 15 % of --dist init's, at ~2k cycles
-  // each; profiles/r06/serve_stages_c10.log)
+  // each; profiles/r06/serve_stages_{normal,init}_c10.log)
   int d = PG_INLINE_FRAME_BOUND ? -1 : plateau_decide<O>(zf, r.e, lane64);
   PG_STAGE(0);
   if (d >= 0) PG_LOG_REQ(1, d);
