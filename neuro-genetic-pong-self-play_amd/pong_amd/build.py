@@ -68,37 +68,48 @@ def _write(path: str, text: str) -> None:
     os.replace(path + ".tmp", path)
 
 
-# Stamps: each object's compile command and the library's whole recipe (every
-# unit's command and the link's), written next to them.  A build input that is
-# not a file -- PG_OFFLOAD_ARCH, HIPCC, the flags above -- changes the command,
-# so an object or library built with another one is rebuilt, not linked into a
-# library labelled with the new arch (round-5 review).
+# Stamps: each object's compile command and the content hash of its inputs
+# (the source, every shared header, this file), and the library's whole recipe,
+# written next to them.  A build input that is not a file -- PG_OFFLOAD_ARCH,
+# HIPCC, the flags above -- changes the command, so an object or library built
+# with another one is rebuilt, not linked into a library labelled with the new
+# arch (round-5 review).  Paths are stamped relative to the repository and
+# inputs by content, not mtime: a copy of the tree elsewhere (the GPU box's
+# snapshot) finds its prebuilt library current instead of rebuilding it.
+def _rel(cmd: list) -> str:
+    return " ".join(cmd).replace(REPO_DIR, "<repo>")
+
+
+def _digest(paths: list) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for path in paths:
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:32]
+
+
 def _unit_stamp(name: str, src: str, extra: list) -> str:
-    return " ".join(_unit_cmd(os.path.join(CSRC, src), extra, _obj(name)))
+    inputs = [os.path.join(CSRC, src), os.path.abspath(__file__)] + HEADERS
+    return _rel(_unit_cmd(os.path.join(CSRC, src), extra, _obj(name))) + " #" + _digest(inputs)
 
 
 def _lib_stamp() -> str:
     lines = [_unit_stamp(name, src, extra) for name, src, extra in sorted(UNITS)]
-    lines.append(" ".join(_link_cmd([_obj(name) for name, _, _ in UNITS], LIB_PATH)))
+    lines.append(_rel(_link_cmd([_obj(name) for name, _, _ in UNITS], LIB_PATH)))
     return "\n".join(lines) + "\n"
 
 
 def _stale(name: str, src: str, extra: list) -> bool:
-    """An object is rebuilt when it is missing, older than its source, any
-    shared header or this file (headers are not tracked per unit), or was
-    compiled by another command."""
+    """An object is rebuilt when it is missing or its stamp differs: another
+    command, or another content of its source, any shared header or this file
+    (headers are not tracked per unit)."""
     obj = _obj(name)
-    if not os.path.exists(obj) or _read(obj + ".stamp") != _unit_stamp(name, src, extra):
-        return True
-    t = os.path.getmtime(obj)
-    return any(os.path.getmtime(d) > t for d in [os.path.join(CSRC, src), os.path.abspath(__file__)] + HEADERS)
+    return not os.path.exists(obj) or _read(obj + ".stamp") != _unit_stamp(name, src, extra)
 
 
 def needs_build() -> bool:
-    if not os.path.exists(LIB_PATH) or _read(LIB_PATH + ".stamp") != _lib_stamp():
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    return not os.path.exists(LIB_PATH) or _read(LIB_PATH + ".stamp") != _lib_stamp()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
