@@ -24,4 +24,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/
 bash tools/pmc_sq.sh $TAG/sq 8 || exit 1
 python3 tools/pmc_summary.py $OUT/sq > $OUT/sq_summary.txt 2>&1 || exit 1
 timeout -k 10 600 python3 -u tools/scale_model.py 8 4 > $OUT/scale_model.log 2>&1 || exit 1
+sha256sum neuro-genetic-pong-self-play_amd/libpong_ga.so >> $OUT/lib_sha.txt  # unchanged: nothing rebuilt it
 echo done > $OUT/ok
