@@ -145,6 +145,7 @@ def main():
     ga.ev.horizon = args.horizon  # pg_eval_args.horizon: 0 = evaluate()'s episodes
     ga.order_by_length = os.environ.get("PG_NO_LENGTH_ORDER") != "1"  # A/B switch for the evaluation order
     ga.early_prep = os.environ.get("PG_NO_EARLY_PREP") != "1"  # A/B switch: schedule + genome records during the HoF scan
+    ga.prepare_first = os.environ.get("PG_NO_PREPARE_FIRST") != "1"  # A/B switch: the HoF prepare before the side stream's work
     # config 5 (strong scaling): contiguous shards.  Length-balanced shards
     # (DeviceGA.balance_shards, PG_BALANCE=1) measured no better at P = 65 536:
     # 8 192 genomes a rank already even out (straggler factor 1.0016 contiguous

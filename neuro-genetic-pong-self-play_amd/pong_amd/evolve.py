@@ -109,7 +109,12 @@ class DeviceGA:
         # across the store/spare swaps; member j's row is _hall_buf[hof_slot[j]]
         self.in_place_hall = True
         self._hall_buf = self.store[: self.H]
-        self.hof_slot = torch.arange(max(self.H, 1), dtype=torch.int32, device=self.device)
+        # the scan's upload lands here (fitness bits, sources, slots); its last
+        # quarter is hof_slot itself, so the new slots need no copy of their own
+        M = max(self.H, 1)
+        self._up_dev = torch.zeros(4 * M, dtype=torch.int32, device=self.device)
+        self.hof_slot = self._up_dev[3 * M:]
+        self.hof_slot.copy_(torch.arange(M, dtype=torch.int32, device=self.device))
         self._hof_slot_h = np.zeros(0, np.int32)
         self._slots_identity = True
         self._up_keep = None
@@ -153,6 +158,9 @@ class DeviceGA:
         # hall-of-fame update on a second HIP stream (False: one stream, the A/B)
         self.side_stream = True
         self._side = None
+        # the hall-of-fame prepare enqueued before the side stream's work (the
+        # host's dispatch of that work then overlaps the device's prepare)
+        self.prepare_first = True
         # sharded variation (module docstring; fused path): at N = 1 the shard is
         # the whole population and there is nothing to leave out
         self.shard_vary = self.world > 1
@@ -785,18 +793,23 @@ class DeviceGA:
         # on this generation's fitness: on a side stream from here, beside the
         # candidates' prepare, the host scan and the commit (the buffers are
         # disjoint: they write store[H:], the update reads rows and store[:old_n]
-        # and writes dst[:m]); the next evaluation waits for both streams
+        # and writes dst[:m]); the next evaluation waits for both streams.  The
+        # prepare and its copy are enqueued first, so the device runs them while
+        # the host enqueues the side stream's work
         main = torch.cuda.current_stream(self.device)
-        side = None
+        side = ready = None
         if overlap and self.side_stream:
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
             side = self._side
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                overlap()
-            overlap = None
-            self._keep_on(main)
+            ready = torch.cuda.Event()
+            ready.record(main)
+            if not self.prepare_first:  # (the A/B: the side stream's work enqueued first)
+                side.wait_event(ready)
+                with torch.cuda.stream(side):
+                    overlap()
+                self._keep_on(main)
+                overlap = None
         n = old_n + k
         cand, cand_fit = cand[:k], cand_fit[:k]
         cand_hash = self._buf("cand_hash", k, torch.int64)
@@ -808,8 +821,14 @@ class DeviceGA:
         copied = torch.cuda.Event()
         copied.record()
         self._mark("hof_prepare", sub=True)  # (profiling only: these marks synchronise)
-        if overlap:
+        if overlap and side is not None:
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                overlap()
+            self._keep_on(main)
+        elif overlap:
             overlap()
+        if overlap:
             self._mark("next_select_vary", sub=True)
         copied.synchronize()
         # the scan straight on the device's packing, visiting only the hall's
@@ -822,13 +841,13 @@ class DeviceGA:
         src, new_fit = res[0], res[1]
         self._mark("hof_scan", sub=True)
         m = src.shape[0]
-        up_d = up.to(self.device, non_blocking=True)
+        up_d = self._up_dev
+        up_d.copy_(up, non_blocking=True)  # (in place: the slots land in hof_slot)
         src_d, fit_d = up_d[2 * M:2 * M + m], up_d[: 2 * M].view(torch.float64)[:m]
         if in_place:
             slot_d = up_d[3 * M:3 * M + m]
             D.hof_commit(self._hall_buf, None, rows, cand, src_d, old_n, self.G, self.hof_hash, cand_hash,
                          self._hof_hash_alt, fit_d, self._hof_fitness_alt, dst_slot=slot_d)
-            self.hof_slot[:m].copy_(slot_d)
             self._hof_slot_h = res[2]
             self._slots_identity = False
         else:
