@@ -161,6 +161,9 @@ class DeviceGA:
         # the hall-of-fame prepare enqueued before the side stream's work (the
         # host's dispatch of that work then overlaps the device's prepare)
         self.prepare_first = True
+        # unsharded: the next generation's side-stream work enqueued behind the
+        # merge, before the host waits on it (_step_fused)
+        self.presubmit = True
         # sharded variation (module docstring; fused path): at N = 1 the shard is
         # the whole population and there is nothing to leave out
         self.shard_vary = self.world > 1
@@ -755,6 +758,12 @@ class DeviceGA:
                worst: Optional[float]):
         """pg_ga_merge_fitness + the generation's first sync: (new fitness,
         candidates, their fitness, stats, nevals, k)."""
+        new_fit, cand, cand_fit, ev = self._merge_start(fit, inv, inherited, worst)
+        return (new_fit, cand, cand_fit) + self._merge_finish(ev)
+
+    def _merge_start(self, fit, inv, inherited, worst):
+        """pg_ga_merge_fitness enqueued with its summary's copy: (new fitness,
+        candidates, their fitness, the event after the copy)."""
         new_fit = self._fit_alt
         cand = self._buf("cand", self.P, torch.int32)
         cand_fit = self._buf("cand_fit", self.P, torch.float64)
@@ -763,13 +772,17 @@ class DeviceGA:
         self._summary_h.copy_(summ, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
+        return new_fit, cand, cand_fit, ev
+
+    def _merge_finish(self, ev):
+        """The generation's first sync: (stats, nevals, k) from the summary."""
         ev.synchronize()
         v = self._summary_h.tolist()
         if v[0]:
             # a NaN fitness is a game whose calculate_reward divided by zero (utils.py:106-108)
             raise ZeroDivisionError("float division by zero (calculate_reward with total_frames == 0)")
         self._fit_alt = self.fitness
-        return new_fit, cand, cand_fit, v[1:5], int(v[5]), int(v[6])
+        return v[1:5], int(v[5]), int(v[6])
 
     def _hof_update_fused(self, rows: torch.Tensor, cand: torch.Tensor, cand_fit: torch.Tensor, k: int,
                           dst: torch.Tensor, overlap=None):
@@ -896,7 +909,22 @@ class DeviceGA:
         self._next = None
         self._mark("select_vary")
         fit = self._evaluate_fused(g, off, order, sched)  # invalid_ind only: clones keep their parent's fitness
-        new_fit, cand, cand_fit, stats, nevals, k = self._merge(fit, inv, inherited, worst)
+        new_fit, cand, cand_fit, merged = self._merge_start(fit, inv, inherited, worst)
+        # Unsharded, the next generation's select/vary/inherit/order/early prep
+        # need only this merge's fitness: enqueued on the side stream now,
+        # behind the merge, while this evaluation still runs -- the device
+        # starts them the moment the merge ends, and the host's dispatch of
+        # them is off the path between two evaluations.  (Sharded, they follow
+        # the candidates' completion, which needs the candidate count.)
+        early_side = self.side_stream and self.presubmit and not self._sharded()
+        if early_side:
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            self._side.wait_event(merged)
+            with torch.cuda.stream(self._side):
+                self._next_gen_prep(g + 1, off, new_fit, self.store, None)
+            self._keep_on(torch.cuda.current_stream(self.device))
+        stats, nevals, k = self._merge_finish(merged)
         self._mark("evaluate")
         cand_pairs = None
         if self._sharded():
@@ -912,7 +940,10 @@ class DeviceGA:
         # store[H:] (this generation's parents, free now), the buffer the swap
         # below makes next step's spare[H:]
         self._hof_update_fused(off, cand, cand_fit, k, self.spare,
-                               overlap=lambda: self._next_gen_prep(g + 1, off, new_fit, self.store, cand_pairs))
+                               overlap=None if early_side else
+                               (lambda: self._next_gen_prep(g + 1, off, new_fit, self.store, cand_pairs)))
+        if early_side:  # the next evaluation follows the side stream's work
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
         self._mark("hall_of_fame")
         self.fitness = new_fit
         self.store, self.spare = self.spare, self.store
