@@ -306,9 +306,11 @@ typedef struct pg_ga_args {
    * candidates and the next selection's parents. */
   const uint8_t *pair_mask;
   /* ABI 10: or a compact list of the pairs to vary -- pair_list[0 .. *pair_count)
-   * (device; pair_cap >= *pair_count bounds the launch) -- so a completion that
-   * varies a few thousand of P / 2 pairs launches that many waves, not one per
-   * pair.  Only the listed pairs' rows and invalid flags are written (pair_mask
+   * (device) -- so a completion that varies a few thousand of P / 2 pairs
+   * launches that many waves, not one per pair.  pair_cap only sizes the grid
+   * (min(pair_cap, pairs, 8192) waves, which stride over the list: since ABI
+   * 12 every listed pair is written whatever pair_cap >= 1 is, so a caller
+   * that knows the count only on the device passes an upper bound).  Only the listed pairs' rows and invalid flags are written (pair_mask
    * is then ignored); pg_ga_list_pairs turns a mask into such a list. */
   const int32_t *pair_list;
   const int32_t *pair_count;

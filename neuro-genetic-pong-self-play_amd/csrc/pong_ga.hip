@@ -387,13 +387,24 @@ __device__ __forceinline__ double rng_u01(uint64_t key, uint64_t b) {
 // sweeps the genes 128 at a time (two coalesced 512-B pieces per parent row,
 // all four loads issued before the arithmetic).
 template <typename WT>
+__device__ __forceinline__ void vary_pair(const pg_ga_args &a, int pair);
+
+template <typename WT>
 __global__ __launch_bounds__(256) void k_vary(pg_ga_args a) {
-  const int pairs = (a.n + 1) / 2;
-  int pair = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (a.pair_list) {  // a compact list of the pairs to write (pong_ga.h)
-    if (pair >= __builtin_amdgcn_readfirstlane(*a.pair_count)) return;
-    pair = __builtin_amdgcn_readfirstlane(a.pair_list[pair]);
+  const int wave = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (a.pair_list) {  // a compact list of the pairs to write (pong_ga.h): the grid strides over it
+    const int count = __builtin_amdgcn_readfirstlane(*a.pair_count);
+    const int waves = (int)gridDim.x * 4;
+#pragma unroll 1
+    for (int w = wave; w < count; w += waves) vary_pair<WT>(a, __builtin_amdgcn_readfirstlane(a.pair_list[w]));
+    return;
   }
+  vary_pair<WT>(a, wave);
+}
+
+template <typename WT>
+__device__ __forceinline__ void vary_pair(const pg_ga_args &a, int pair) {
+  const int pairs = (a.n + 1) / 2;
   if (pair >= pairs) return;
   const int lane = threadIdx.x & 63;
   const int i0 = 2 * pair, i1 = 2 * pair + 1;
@@ -1054,7 +1065,11 @@ int32_t pg_ga_vary(const pg_ga_args *a, void *stream) {
   if (a->n == 0) return PG_OK;
   const int pairs = (a->n + 1) / 2;
   if (a->pair_list && (!a->pair_count || a->pair_cap < 0)) return fail(PG_ERR_INVALID, "varAnd: pair_list needs pair_count and pair_cap >= 0");
-  const int waves = a->pair_list ? (a->pair_cap < pairs ? a->pair_cap : pairs) : pairs;
+  // list mode: the grid strides over the listed pairs, so pair_cap (an upper
+  // bound of the count, which the device holds) only sizes the grid
+  constexpr int kListWaves = 8192;
+  int waves = a->pair_list ? (a->pair_cap < pairs ? a->pair_cap : pairs) : pairs;
+  if (a->pair_list && waves > kListWaves) waves = kListWaves;
   if (waves == 0) return PG_OK;
   const dim3 grid((unsigned)((waves + 3) / 4));  // one wave per pair
   if (a->dtype == PG_F64)

@@ -910,24 +910,39 @@ class DeviceGA:
         self._mark("select_vary")
         fit = self._evaluate_fused(g, off, order, sched)  # invalid_ind only: clones keep their parent's fitness
         new_fit, cand, cand_fit, merged = self._merge_start(fit, inv, inherited, worst)
-        # Unsharded, the next generation's select/vary/inherit/order/early prep
-        # need only this merge's fitness: enqueued on the side stream now,
-        # behind the merge, while this evaluation still runs -- the device
-        # starts them the moment the merge ends, and the host's dispatch of
-        # them is off the path between two evaluations.  (Sharded, they follow
-        # the candidates' completion, which needs the candidate count.)
-        early_side = self.side_stream and self.presubmit and not self._sharded()
+        # The next generation's select/vary/inherit/order/early prep need only
+        # this merge's fitness (and, sharded, the candidates' completion): they
+        # are enqueued on the side stream now, behind the merge, while this
+        # evaluation still runs -- the device starts them the moment the merge
+        # ends, and the host's dispatch of them is off the path between two
+        # evaluations.  Sharded, the candidates' completion goes first on the
+        # main stream, over the candidate list bounded by the count the merge
+        # left on the device (rows past it read -1, which marks no pair).
+        early_side = self.side_stream and self.presubmit and not self._balanced()
+        cand_pairs = None
         if early_side:
+            main = torch.cuda.current_stream(self.device)
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
-            self._side.wait_event(merged)
+            after = merged
+            if self._sharded():
+                if self.H:
+                    if getattr(self, "_iota_P", None) is None:
+                        self._iota_P = torch.arange(self.P, dtype=torch.float64, device=self.device)
+                    k_dev = self._buf("summary", 8, torch.float64)[6]
+                    rows_all = torch.where(self._iota_P < k_dev, cand, torch.full_like(cand, -1))
+                else:
+                    rows_all = cand[:0]  # (no hall of fame: the candidates are never read)
+                cand_pairs = self._complete(g, off, self._rows, rows_all, "cand")
+                after = torch.cuda.Event()
+                after.record(main)
+            self._side.wait_event(after)
             with torch.cuda.stream(self._side):
-                self._next_gen_prep(g + 1, off, new_fit, self.store, None)
-            self._keep_on(torch.cuda.current_stream(self.device))
+                self._next_gen_prep(g + 1, off, new_fit, self.store, cand_pairs)
+            self._keep_on(main)
         stats, nevals, k = self._merge_finish(merged)
         self._mark("evaluate")
-        cand_pairs = None
-        if self._sharded():
+        if self._sharded() and not early_side:
             # the candidates' rows of this offspring beyond the shard (the update
             # hashes and gathers them); the next selection's parents follow on
             # the side stream (_next_gen_prep), both before generation g + 1's
