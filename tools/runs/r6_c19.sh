@@ -1,6 +1,5 @@
 # round 6: bench.py's N = 2 launch (2 gloo ranks sharing the one GPU) with the
 # sharded presubmit on and off, alternating, three each (is the c18 gap real?),
-# and the same at N = 1 over RCCL (PG_FORCE_DIST=1, sharded path off).
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${RUN:-r6_c19}
