@@ -190,3 +190,24 @@ def test_struct_size_refuses_other_layouts(lib):
     old.n_games, old.n_genomes = 6, 0
     rc = lib.pg_eval_population(ctypes.cast(ctypes.byref(old), ctypes.POINTER(_lib.PgEvalArgs)), None)
     assert rc == _lib.PG_ERR_INVALID and b"struct_size=3" in lib.pg_last_error()
+
+
+def test_build_stamps_are_relocatable(tmp_path):
+    """The library's build stamp names no absolute path and no mtime: a copy
+    of the tree elsewhere (the GPU box's snapshot, without the objects) finds
+    its prebuilt libpong_ga.so current and loads it instead of rebuilding."""
+    import shutil
+    from pong_amd import _lib, build
+    if build.needs_build():
+        pytest.skip("the library is not built here")
+    stamp = open(_lib.LIB_PATH + ".stamp").read()
+    assert _lib.REPO_DIR not in stamp and "<repo>" in stamp
+    dst = tmp_path / "copy"
+    repo = _lib.REPO_DIR
+    ignore = shutil.ignore_patterns(".git", "gpurun_out", "*.o", "__pycache__", "profiles", "ab", "variants")
+    shutil.copytree(repo, dst, ignore=ignore, symlinks=True)
+    code = ("import sys; sys.path.insert(0, %r); from pong_amd import build as B; "
+            "print(B.needs_build())" % str(dst / "neuro-genetic-pong-self-play_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "False"
