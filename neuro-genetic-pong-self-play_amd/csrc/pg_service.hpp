@@ -78,7 +78,7 @@ __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, In
   float zf[O];
 #pragma unroll
   for (int o = 0; o < O; ++o) zf[o] = r.z[o];
-#ifdef PG_INLINE_LOG  // diagnostic build: one record per request in p.hard_log {z0..z3, e, frame bound, stage | idx << 8, 0}
+#ifdef PG_INLINE_LOG  // diagnostic build: one record per request in p.hard_log {z0..z3, e, frame bound, stage | idx << 8 | wave << 16, network}
   float ef_log = -1.f;
   const auto log_req = [&](int stage, int idx) {
     if (p.hard_log && p.counters && lane64 == 0) {
@@ -88,8 +88,9 @@ __device__ __forceinline__ int serve_inline(const EvalParams &p, const WT *g, In
         for (int o = 0; o < 4; ++o) rec[o] = __float_as_uint(o < O ? zf[o] : 0.f);
         rec[4] = __float_as_uint(r.e);
         rec[5] = __float_as_uint(ef_log);
-        rec[6] = (uint32_t)stage | ((uint32_t)(idx & 255) << 8);
-        rec[7] = 0;
+        rec[6] = (uint32_t)stage | ((uint32_t)(idx & 255) << 8) |
+                 ((uint32_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) << 16);
+        rec[7] = (uint32_t)((uint64_t)g >> 3);  // the network (its genome row's address / 8)
       }
     }
   };

@@ -62,7 +62,8 @@ def main(out, gens=3, dist="uniform"):
     z = rec[:, :4].view(np.float32)
     e, ef = rec[:, 4].view(np.float32), rec[:, 5].view(np.float32)
     stage, idx = rec[:, 6] & 255, (rec[:, 6] >> 8) & 255
-    np.savez_compressed(out, z=z, e=e, ef=ef, stage=stage, idx=idx, counters=c)
+    wave, net = rec[:, 6] >> 16, rec[:, 7]
+    np.savez_compressed(out, z=z, e=e, ef=ef, stage=stage, idx=idx, wave=wave, net=net, counters=c)
     fwd = c[1]
     print(f"forwards {fwd}, certificate failures {c[4]} ({c[4] / fwd:.4f}), in-wave {c[6]}, f64-certified {c[5]}, "
           f"numpy-order {c[2]}, serve_inline requests {c[9]} ({c[9] / fwd:.5f} of forwards)")
@@ -74,6 +75,26 @@ def main(out, gens=3, dist="uniform"):
         if m.any():
             print(f"stage {s} {name}: {m.sum()}  top1 pct {np.percentile(top1[m], [5, 50, 95]).round(3)}  "
                   f"gap pct {np.percentile((top1 - top2)[m], [5, 50, 95])}  e med {np.median(e[m]):.3g}")
+    # locality: of each wave's requests (log order is each wave's serving order),
+    # how many repeat a network among that wave's last K requests -- what a
+    # per-wave cache of the f64 genome values would hit
+    for K in (1, 2, 4, 8):
+        hits = tot = 0
+        for wv in np.unique(wave):
+            seq = net[wave == wv]
+            for i in range(len(seq)):
+                tot += 1
+                hits += int(seq[i] in seq[max(0, i - K):i])
+        print(f"requests repeating one of the wave's last {K} networks: {hits} of {tot} ({hits / max(tot, 1):.3f})")
+    f3 = stage == 3
+    for K in (1, 4):
+        hits = tot = 0
+        for wv in np.unique(wave[f3]):
+            seq = net[f3 & (wave == wv)]
+            for i in range(len(seq)):
+                tot += 1
+                hits += int(seq[i] in seq[max(0, i - K):i])
+        print(f"f64-stage requests repeating one of the wave's last {K} f64-stage networks: {hits} of {tot} ({hits / max(tot, 1):.3f})")
     bands = [(-1e9, 0), (0, 22.2), (22.2, 30), (30, 36.7), (36.7, 1e9)]
     for lo, hi in bands:
         m = (top1 >= lo) & (top1 < hi)
