@@ -1287,10 +1287,14 @@ int32_t pg_hof_update_packed(const pg_hof_packed_args *a) {
   if (a->maxsize < 0 || hn < 0 || hn > a->maxsize || k < 0 || !a->new_n || (a->maxsize > 0 && (!a->new_src || !a->new_fitness)) ||
       (hn > 0 && !a->hof_fitness) || (hn + k > 0 && !a->packed))
     return fail(PG_ERR_INVALID, "hof_update_packed: bad sizes or NULL buffers");
-  if (a->slot_in)
-    for (int e = 0; e < hn; ++e)
-      if (a->slot_in[e] < 0 || a->slot_in[e] >= hn)
-        return fail(PG_ERR_INVALID, "hof_update_packed: slot_in[%d]=%d outside [0, hof_n)", e, a->slot_in[e]);
+  if (a->slot_in && hn > 0) {  // (a min/max pass the compiler vectorises: the scan is on the generation's path)
+    int32_t lo = a->slot_in[0], hi = a->slot_in[0];
+    for (int e = 1; e < hn; ++e) {
+      lo = a->slot_in[e] < lo ? a->slot_in[e] : lo;
+      hi = a->slot_in[e] > hi ? a->slot_in[e] : hi;
+    }
+    if (lo < 0 || hi >= hn) return fail(PG_ERR_INVALID, "hof_update_packed: slot_in outside [0, hof_n) (%d..%d)", lo, hi);
+  }
   const int64_t *pk = a->packed;
   const int n = hn + k;
   auto rank_of = [&](int e) { return (int32_t)(uint32_t)pk[e]; };

@@ -164,6 +164,7 @@ class DeviceGA:
         # unsharded: the next generation's side-stream work enqueued behind the
         # merge, before the host waits on it (_step_fused)
         self.presubmit = True
+        self._iota_P = None  # (sharded presubmit: row positions, to bound the candidate list on the device)
         # sharded variation (module docstring; fused path): at N = 1 the shard is
         # the whole population and there is nothing to leave out
         self.shard_vary = self.world > 1
@@ -927,7 +928,7 @@ class DeviceGA:
             after = merged
             if self._sharded():
                 if self.H:
-                    if getattr(self, "_iota_P", None) is None:
+                    if self._iota_P is None:
                         self._iota_P = torch.arange(self.P, dtype=torch.float64, device=self.device)
                     k_dev = self._buf("summary", 8, torch.float64)[6]
                     rows_all = torch.where(self._iota_P < k_dev, cand, torch.full_like(cand, -1))

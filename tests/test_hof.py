@@ -284,3 +284,20 @@ def test_hof_update_packed_slots_large_out_buffer():
     _check_slots(slots, np.arange(H, dtype=np.int64), src, new_slots, H)
     with pytest.raises(ValueError):
         D.hof_update_packed(H, hof_f, packed, k, out=np.zeros(4 * H - 1, np.int32))
+
+
+def test_hof_update_packed_refuses_bad_slots():
+    """slot_in outside [0, hof_n) is refused before any slot is handed out
+    (the commit would write the hall's storage at those slots)."""
+    rng = np.random.default_rng(5)
+    H = 16
+    hof_f = np.sort(rng.normal(size=H))[::-1].copy()
+    hof_h = rng.integers(-2**62, 2**62, size=H)
+    fit = rng.normal(size=4) + 3.0
+    hsh = rng.integers(-2**62, 2**62, size=4)
+    packed = _packing(hof_f, hof_h, fit, hsh)
+    for bad in (-1, H):
+        slots = np.arange(H, dtype=np.int32)
+        slots[7] = bad
+        with pytest.raises(RuntimeError):
+            D.hof_update_packed(H, hof_f, packed, 4, slot_in=slots, slots=True)
