@@ -106,7 +106,8 @@ def test_init_population_generations_every_row_against_oracle(gpu, oracle):
     of forwards (bench.py --dist init) and so drive the whole decision cascade
     (in-wave rules, the frame bound, the f64 stage, numpy's order): DeviceGA at
     population 4 096 against a full hall of U[0, 1) genomes, and every played
-    row of the fourth evaluation re-played by the oracle, bit-exact."""
+    row of the fourth evaluation re-played by the oracle, bit-exact; then 512
+    of those rows and games in the fixed-horizon mode against the oracle's."""
     from pong_amd.evolve import DeviceGA
     shape = [6, 64, 3]
     P = 4096
@@ -143,6 +144,22 @@ def test_init_population_generations_every_row_against_oracle(gpu, oracle):
     np.testing.assert_array_equal(s["fitness"], ref["fitness"])
     np.testing.assert_array_equal(s["frames"], ref["frames"])
     np.testing.assert_array_equal(s["scores"], ref["scores"])
+    # the fixed-horizon instance (its own inline decision path) on the same
+    # evolved genomes and games: 512 rows, T = 400 frames per slot, vs the oracle
+    from pong_amd.device import Evaluator
+    m, T = 512, 400
+    ev = Evaluator(shape, device=gpu, horizon=T)
+    opp_t = torch.tensor(s["opp"][:m], device=gpu)
+    res_h, _ = ev.evaluate(torch.tensor(s["genomes"][:m], device=gpu), torch.tensor(s["kind"][:m], device=gpu),
+                           opp_t, torch.tensor(s["mult"][:m], device=gpu),
+                           opponents=torch.tensor(s["opponents"], device=gpu))
+    torch.cuda.synchronize()
+    ch = res_h.counters.cpu().numpy().astype(np.int64)
+    assert ch[4] > 0.05 * ch[1], "expected the horizon instance to meet the population's certificate failures"
+    ref_h = oracle.eval_population(s["genomes"][:m], shape, s["kind"][:m], s["opp"][:m], s["mult"][:m],
+                                   opponents=s["opponents"], n_threads=16, horizon=T)
+    for name in ("scores", "frames", "total_frames", "rewards", "fitness"):
+        np.testing.assert_array_equal(getattr(res_h, name).cpu().numpy(), ref_h[name], err_msg=name)
 
 
 def test_config5_wide_pop65536(gpu, oracle):
