@@ -147,6 +147,7 @@ def main():
     ga.early_prep = os.environ.get("PG_NO_EARLY_PREP") != "1"  # A/B switch: schedule + genome records during the HoF scan
     ga.prepare_first = os.environ.get("PG_NO_PREPARE_FIRST") != "1"  # A/B switch: the HoF prepare before the side stream's work
     ga.presubmit = os.environ.get("PG_NO_PRESUBMIT") != "1"  # A/B switch: the next generation's side work enqueued before the merge sync
+    ga.persistent_bufs = os.environ.get("PG_NO_PERSIST") != "1"  # A/B switch: schedule/invalid/remap buffers kept
     # config 5 (strong scaling): contiguous shards.  Length-balanced shards
     # (DeviceGA.balance_shards, PG_BALANCE=1) measured no better at P = 65 536:
     # 8 192 genomes a rank already even out (straggler factor 1.0016 contiguous

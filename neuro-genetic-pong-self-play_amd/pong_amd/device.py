@@ -459,16 +459,23 @@ SCHEDULES = {"reference": L.PG_SCHED_REFERENCE, "selfplay": L.PG_SCHED_SELFPLAY}
 
 def schedule(mode: str, n: int, n_games: int, row_offset: int, hof_fitness: Optional[torch.Tensor], n_hof: int,
              seed: int, generation: int, device, rows: Optional[torch.Tensor] = None, hof_slices: int = 1,
-             block_rows: int = 0, slice_local: bool = False):
-    """pg_ga_schedule: (kind, opp, mult) [n, n_games] of evaluate()'s games on device;
+             block_rows: int = 0, slice_local: bool = False, out: Optional[tuple] = None):
+    """pg_ga_schedule: (kind, opp, mult) [n, n_games] of evaluate()'s games on device
+    (``out``: the three tensors to write, else fresh ones);
     ``rows`` ([n] int32) gives entry i's global population row (default row_offset + i).
     Self-play with ``hof_slices`` K > 1: the genomes of row block r // block_rows
     play the hall's interleaved slice (r // block_rows) mod K (pong_ga.h); with
     ``slice_local`` opp indexes the slice (pass ``hall[b::K]`` as the opponents)."""
     dev = torch.device(device)
-    kind = torch.empty((n, n_games), dtype=torch.int32, device=dev)
-    opp = torch.empty((n, n_games), dtype=torch.int32, device=dev)
-    mult = torch.empty((n, n_games), dtype=torch.float64, device=dev)
+    if out is None:
+        kind = torch.empty((n, n_games), dtype=torch.int32, device=dev)
+        opp = torch.empty((n, n_games), dtype=torch.int32, device=dev)
+        mult = torch.empty((n, n_games), dtype=torch.float64, device=dev)
+    else:
+        kind, opp, mult = out
+        _need(kind, "kind", torch.int32, dev, (n, n_games))
+        _need(opp, "opp", torch.int32, dev, (n, n_games))
+        _need(mult, "mult", torch.float64, dev, (n, n_games))
     if hof_fitness is not None:
         _need(hof_fitness, "hof_fitness", torch.float64, dev)
         if hof_fitness.numel() < n_hof:

@@ -164,6 +164,11 @@ class DeviceGA:
         # unsharded: the next generation's side-stream work enqueued behind the
         # merge, before the host waits on it (_step_fused)
         self.presubmit = True
+        self._pinned = {}  # name -> persistent pinned host buffer (_pin)
+        # the schedule, invalid flags and remapped opponents in persistent
+        # buffers (False: fresh tensors each generation, the A/B)
+        self.persistent_bufs = True
+        self._up_flip = 0
         self._iota_P = None  # (sharded presubmit: row positions, to bound the candidate list on the device)
         # sharded variation (module docstring; fused path): at N = 1 the shard is
         # the whole population and there is nothing to leave out
@@ -215,7 +220,8 @@ class DeviceGA:
         hall's local indices need nothing: its rows were gathered in order)."""
         if not self._in_place() or not n_hof or self._sliced(n_hof) or self._slots_identity:
             return opp
-        return torch.index_select(self.hof_slot[:n_hof], 0, opp.reshape(-1)).view_as(opp)
+        out = self._buf("opp_slots", opp.numel(), torch.int32) if self.persistent_bufs else None
+        return torch.index_select(self.hof_slot[:n_hof], 0, opp.reshape(-1), out=out).view_as(opp)
 
     def _opponents_by_position(self, n_hof: int) -> Optional[torch.Tensor]:
         """The opponents in the schedule's index order (for on_evaluate)."""
@@ -225,11 +231,11 @@ class DeviceGA:
             return self.hall_of_fame[:n_hof]
         return self._opponents(self.store, n_hof)
 
-    def eval_schedule(self, g: int, n_hof: Optional[int] = None, rows="last"):
+    def eval_schedule(self, g: int, n_hof: Optional[int] = None, rows="last", out: Optional[tuple] = None):
         """(kind, opp, mult) of generation g's games for this rank's shard,
         as the evaluation plays them (opp indexes the opponents the evaluation
         passes -- the hall, or this rank's slice of it; rows: the evaluation
-        order, by default the last evaluation's)."""
+        order, by default the last evaluation's; out: the tensors to write)."""
         n_hof = self.hof_n if n_hof is None else n_hof
         rows = self.last_rows if isinstance(rows, str) else rows
         kw = {}
@@ -237,7 +243,17 @@ class DeviceGA:
             kw = dict(hof_slices=self.hof_slices, block_rows=self.hof_block_rows, slice_local=self._sliced(n_hof))
         n = rows.shape[0] if rows is not None else self.hi - self.lo
         return D.schedule(self.schedule, n, self.n_games, self.lo, self.hof_fitness, n_hof, self.seed,
-                          g, self.device, rows=rows, **kw)
+                          g, self.device, rows=rows, out=out, **kw)
+
+    def _sched_bufs(self, g: int, n: int) -> tuple:
+        """Generation g's schedule tensors, by generation parity (the next
+        generation's schedule is made while this one's evaluation may still
+        read it); persistent, so no side-stream allocation is freed across streams."""
+        if not self.persistent_bufs:
+            return None
+        return (self._buf("sched_kind%d" % (g & 1), (n, self.n_games), torch.int32),
+                self._buf("sched_opp%d" % (g & 1), (n, self.n_games), torch.int32),
+                self._buf("sched_mult%d" % (g & 1), (n, self.n_games), torch.float64))
 
     def _balanced(self) -> bool:
         # (not with a sliced hall: there a rank's opponents are its row block's slice)
@@ -677,7 +693,8 @@ class DeviceGA:
                            exclude=cand_pairs if prev is None else (cand_pairs | prev))
         _, inv = D.vary(parents, chosen, self.G, self.cxpb, self.mutpb, self.alpha, self.mu, self.sigma, self.indpb,
                         seed=self.seed, generation=g, out=store[self.H:],
-                        pair_mask=self._shard_mask() if self._sharded() else None)
+                        pair_mask=self._shard_mask() if self._sharded() else None,
+                        invalid=self._buf("invalid%d" % (g & 1), self.P, torch.uint8) if self.persistent_bufs else None)
         inherited = self._buf("inherited", self.P, torch.float64)
         D.inherit(chosen, fitness, inherited, self.lineage_frames, self._lineage_alt)
         self.lineage_frames, self._lineage_alt = self._lineage_alt, self.lineage_frames
@@ -700,7 +717,7 @@ class DeviceGA:
                 or self.last.fitness.shape[0] != n):
             return None
         local, count = order
-        sched = self.eval_schedule(g, n_hof=self.H, rows=local)
+        sched = self.eval_schedule(g, n_hof=self.H, rows=local, out=self._sched_bufs(g, n))
         # the records land in the evaluator's workspace; the later PG_PREP_REST call
         # (same genomes, rows, count; opponents of the same size) adds the opponents'
         # (the opponents' rows are not read by a "genomes" preparation: the
@@ -726,7 +743,7 @@ class DeviceGA:
         n = self._n_eval
         local, count = order
         if sched is None:
-            kind, opp, mult = self.eval_schedule(g, rows=local)
+            kind, opp, mult = self.eval_schedule(g, rows=local, out=self._sched_bufs(g, n))
         else:  # made during the hall-of-fame scan with the genomes' records (_early_prep)
             kind, opp, mult = sched
         opponents = self._opponents(self.store, self.hof_n)
@@ -830,7 +847,7 @@ class DeviceGA:
         packed = self._buf("packed", n + k, torch.int64)
         D.hof_prepare_cand(self.hof_fitness[:old_n], self.hof_hash[:old_n], cand, cand_fit, rows, self.G, cand_hash,
                            packed, self.ws)
-        packed_h = torch.empty(n + k, dtype=torch.int64, pin_memory=True)
+        packed_h = self._pin("packed", n + k, torch.int64)
         packed_h.copy_(packed, non_blocking=True)
         copied = torch.cuda.Event()
         copied.record()
@@ -847,9 +864,13 @@ class DeviceGA:
         copied.synchronize()
         # the scan straight on the device's packing, visiting only the hall's
         # tail and the candidates (pg_hof_update_packed, O(k log k)); its
-        # outputs land in the pinned upload buffer: fitness, sources, slots
+        # outputs land in the pinned upload buffer: fitness, sources, slots.
+        # Two such buffers alternate: this scan reads the last one's fitness
+        # and slots, and an upload is done long before its buffer's next turn
+        # (the generation in between waits on the device twice)
         M = max(self.H, 1)
-        up = torch.empty(4 * M, dtype=torch.int32, pin_memory=True)
+        self._up_flip ^= 1
+        up = self._pin("up%d" % self._up_flip, 4 * M, torch.int32)
         res = D.hof_update_packed(self.H, self._hof_fit_host, packed_h.numpy(), k, out=up.numpy(),
                                   slot_in=self._hof_slot_h if in_place else None, slots=in_place)
         src, new_fit = res[0], res[1]
@@ -874,6 +895,14 @@ class DeviceGA:
         self._up_keep = up  # _hof_fit_host (and _hof_slot_h) are views of it
         if side is not None:
             main.wait_stream(side)
+
+    def _pin(self, name: str, n: int, dtype) -> torch.Tensor:
+        """A persistent pinned host buffer's first n entries (grown on demand)."""
+        buf = self._pinned.get(name)
+        if buf is None or buf.shape[0] < n or buf.dtype != dtype:
+            buf = torch.empty(max(n, 1), dtype=dtype, pin_memory=True)
+            self._pinned[name] = buf
+        return buf[:n]
 
     def _keep_on(self, stream):
         """The side stream's fresh tensors in self._next are read on ``stream``
