@@ -22,6 +22,8 @@
 //   pg_hof_commit           the new hall: rows, hashes and fitness in one pass
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "pg_eval.hpp"
@@ -247,24 +249,62 @@ __global__ void k_hof_insert(const uint64_t *hof_hash, int hn, Slot *mt, unsigne
   }
 }
 
+// The two searches of k_hof_rank_pack, as first-false of a monotone
+// predicate over a sorted array (true on a prefix).  Every block stages a
+// sample of each array (every s-th element, <= kSamples of them) in LDS; the
+// search runs over the sample, then counts the predicate over the s - 1
+// elements of the one window left -- independent loads, where a binary search
+// over global memory is ~14 dependent ones (this kernel shares the device
+// with the side stream's vary and records, and its slowest thread sets it)
+constexpr int kSamples = 2048;
+
+__device__ inline int sample_stride(int len) { return len > kSamples ? (len + kSamples - 1) / kSamples : 1; }
+
+__device__ inline void stage_samples(double *sh, const double *a, int len, int st) {
+  const int ns = (len + st - 1) / st;
+  for (int i = threadIdx.x; i < ns; i += kT) sh[i] = a[(long)i * st];
+}
+
+// first index m of a[0, len) whose pred(a[m]) is false (len if none)
+template <typename Pred>
+__device__ inline int first_false(const double *sh, const double *a, int len, int st, Pred pred) {
+  const int ns = (len + st - 1) / st;
+  int lo = 0, hi = ns;  // first sample whose predicate is false
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (pred(sh[m])) lo = m + 1; else hi = m;
+  }
+  if (st == 1 || lo == 0) return lo * st < len ? lo * st : len;
+  // the answer lies in ((lo - 1) * st, min(lo * st, len)]
+  const int w0 = (lo - 1) * st + 1, w1 = lo * st < len ? lo * st : len;
+  int c = 0;
+  for (int i = w0; i < w1; ++i) c += pred(a[i]) ? 1 : 0;
+  return w0 + c;
+}
+
 // rank (ascending (fitness, age); members older than every candidate) and
 // dense class of entry e, packed as pg_hof_rank_classes does
-__global__ void k_hof_rank_pack(const double *hof_fitness, const uint64_t *hof_hash, int hn, const double *cand_fitness,
-                                const uint64_t *cand_hash, int k, const double *sorted_fit, const int32_t *sorted_idx,
-                                const Slot *mt, unsigned mcap, const Slot *ct, unsigned ccap, int64_t *packed) {
+__global__ __launch_bounds__(256) void k_hof_rank_pack(const double *hof_fitness, const uint64_t *hof_hash, int hn,
+                                                       const double *cand_fitness, const uint64_t *cand_hash, int k,
+                                                       const double *sorted_fit, const int32_t *sorted_idx,
+                                                       const Slot *mt, unsigned mcap, const Slot *ct, unsigned ccap,
+                                                       int64_t *packed) {
+  __shared__ double sh_cand[kSamples], sh_hof[kSamples];
   const int e = blockIdx.x * kT + threadIdx.x;
   const int n = hn + k;
+  const int st_c = sample_stride(k), st_h = sample_stride(hn);
+  // (block-uniform: which searches this block's entries run)
+  const int b0 = blockIdx.x * kT, b1 = b0 + kT;
+  if (b0 < hn) stage_samples(sh_cand, sorted_fit, k, st_c);
+  if (b1 > hn) stage_samples(sh_hof, hof_fitness, hn, st_h);
+  __syncthreads();
   if (e < k) packed[n + e] = __double_as_longlong(cand_fitness[e]);
   if (e >= n) return;
   int rank, cls;
   if (e < hn) {
     const double f = hof_fitness[e];
     // candidates strictly below f (equal ones are younger: above)
-    int lo = 0, hi = k;
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if (sorted_fit[m] < f) lo = m + 1; else hi = m;
-    }
+    const int lo = first_false(sh_cand, sorted_fit, k, st_c, [f](double x) { return x < f; });
     rank = (hn - 1 - e) + lo;
     cls = table_find(mt, mcap, hof_hash[e]);
   } else {
@@ -274,11 +314,7 @@ __global__ void k_hof_rank_pack(const double *hof_fitness, const uint64_t *hof_h
     const int j = sorted_idx[s];
     const double f = sorted_fit[s];
     // members with fitness <= f: items order is descending, so count those > f
-    int lo = 0, hi = hn;
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if (hof_fitness[m] > f) lo = m + 1; else hi = m;
-    }
+    const int lo = first_false(sh_hof, hof_fitness, hn, st_h, [f](double x) { return x > f; });
     rank = s + (hn - lo);
     const int mm = table_find(mt, mcap, cand_hash[j]);
     cls = mm >= 0 ? mm : hn + table_find(ct, ccap, cand_hash[j]);
@@ -337,24 +373,29 @@ __global__ void k_cand_keys(const double *f, int k, double *keys, int32_t *iota)
   iota[i] = i;
 }
 
+// one wave per hall position, four per block, striding over the positions:
+// the in-place commit copies only the entering candidates' rows, so most
+// waves write two words -- a block per position was mostly launch cost
 template <typename WT>
 __global__ __launch_bounds__(256) void k_hof_commit(WT *dst, int64_t dst_stride, const WT *old_rows, int64_t old_stride,
                                                     const WT *rows, int64_t rows_stride, const int32_t *cand,
-                                                    const int32_t *src, int n_old, int64_t genes,
+                                                    const int32_t *src, int m, int n_old, int64_t genes,
                                                     const uint64_t *old_hash, const uint64_t *cand_hash,
                                                     uint64_t *new_hash, const double *fit_in, double *new_fitness,
                                                     const int32_t *dst_slot) {
-  const int j = blockIdx.x;
-  const int s = src[j];
-  // (dst_slot: the hall in place -- a kept member's row is already in its slot)
-  if (!dst_slot || s >= n_old) {
-    const WT *from = s < n_old ? old_rows + (long)s * old_stride : rows + (long)cand[s - n_old] * rows_stride;
-    WT *to = dst + (long)(dst_slot ? dst_slot[j] : j) * dst_stride;
-    for (int64_t g = threadIdx.x; g < genes; g += 256) to[g] = from[g];
-  }
-  if (threadIdx.x == 0) {
-    new_hash[j] = s < n_old ? old_hash[s] : cand_hash[s - n_old];
-    new_fitness[j] = fit_in[j];
+  const int lane = threadIdx.x & 63;
+  for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < m; j += gridDim.x * 4) {
+    const int s = src[j];
+    // (dst_slot: the hall in place -- a kept member's row is already in its slot)
+    if (!dst_slot || s >= n_old) {
+      const WT *from = s < n_old ? old_rows + (long)s * old_stride : rows + (long)cand[s - n_old] * rows_stride;
+      WT *to = dst + (long)(dst_slot ? dst_slot[j] : j) * dst_stride;
+      for (int64_t g = lane; g < genes; g += 64) to[g] = from[g];
+    }
+    if (lane == 0) {
+      new_hash[j] = s < n_old ? old_hash[s] : cand_hash[s - n_old];
+      new_fitness[j] = fit_in[j];
+    }
   }
 }
 
@@ -525,15 +566,17 @@ int32_t pg_hof_commit(const pg_hof_commit_args *a, void *stream) {
     return fail(PG_ERR_INVALID, "hof_commit: bad sizes, dtype or NULL buffers");
   if (a->m == 0) return PG_OK;
   const hipStream_t s = (hipStream_t)stream;
+  // (a wave per position; 2048 blocks = 8 per CU cover the largest hall in few passes)
+  const dim3 grid((unsigned)std::min<int64_t>(((int64_t)a->m + 3) / 4, 2048));
   if (a->dtype == PG_F64)
-    hipLaunchKernelGGL(k_hof_commit<double>, dim3(a->m), dim3(256), 0, s, (double *)a->dst, a->dst_stride,
+    hipLaunchKernelGGL(k_hof_commit<double>, grid, dim3(256), 0, s, (double *)a->dst, a->dst_stride,
                        (const double *)a->old_rows, a->old_stride, (const double *)a->rows, a->rows_stride, a->cand,
-                       a->src, a->n_old, a->genes, a->old_hash, a->cand_hash,
+                       a->src, (int)a->m, a->n_old, a->genes, a->old_hash, a->cand_hash,
                        a->new_hash, a->fitness_in, a->new_fitness, a->dst_slot);
   else
-    hipLaunchKernelGGL(k_hof_commit<float>, dim3(a->m), dim3(256), 0, s, (float *)a->dst, a->dst_stride,
+    hipLaunchKernelGGL(k_hof_commit<float>, grid, dim3(256), 0, s, (float *)a->dst, a->dst_stride,
                        (const float *)a->old_rows, a->old_stride, (const float *)a->rows, a->rows_stride, a->cand,
-                       a->src, a->n_old, a->genes, a->old_hash, a->cand_hash,
+                       a->src, (int)a->m, a->n_old, a->genes, a->old_hash, a->cand_hash,
                        a->new_hash, a->fitness_in, a->new_fitness, a->dst_slot);
   PG_HIP(hipGetLastError());
   return PG_OK;

@@ -137,10 +137,13 @@ def test_scatter_and_inherit(gpu):
     assert torch.equal(inh, fit_all[chosen.long()]) and torch.equal(lo_out, lineage[chosen.long()])
 
 
-@pytest.mark.parametrize("hn,k,dup", [(0, 50, False), (16, 40, True), (512, 3000, True), (4096, 100, False)])
+@pytest.mark.parametrize("hn,k,dup", [(0, 50, False), (16, 40, True), (512, 3000, True), (4096, 100, False),
+                                      (16384, 5000, True), (20000, 70000, False)])
 def test_hof_prepare_cand_same_scan_as_rank_classes(gpu, hn, k, dup):
     """The candidate-only ranks and table classes feed pg_hof_update the same
-    hall as pg_hof_rank_classes' full sorts (ties and duplicate rows included)."""
+    hall as pg_hof_rank_classes' full sorts (ties and duplicate rows included;
+    the searches' LDS samples are exact up to 2 048 entries, sampled beyond:
+    strides 2, 8 and 35 here)."""
     from pong_amd import device as D
     rng = np.random.default_rng(hn + k)
     G = 20
